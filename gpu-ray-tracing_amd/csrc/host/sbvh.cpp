@@ -1,0 +1,454 @@
+// sbvh.cpp — spatial-split BVH builder.
+//
+// Restates the reference's SplitBVHBuilder (src/rt/bvh/SplitBVHBuilder.cc:55-485,
+// Stich et al. 2009) including the parts that decide output bits: the
+// reference's median-3 quicksort + insertion sort (src/framework/base/Sort.cc:
+// 63-239) with the (centroid sum, triIdx) comparator, the SAH tie-break on
+// i^2 + (n-i)^2, degenerate-reference removal by swap-with-last, the 128-bin
+// spatial search with float->int bin truncation, and the duplicate / unsplit
+// decision. Where the reference kept one global reference stack and built the
+// right child before the left one, this build gives every node its own copy
+// of the segment it owns, which yields the same subtree bits and lets large
+// subtrees build on separate threads.
+#include <algorithm>
+#include <chrono>
+#include <climits>
+#include <cmath>
+#include <thread>
+
+#include "bvh.hpp"
+
+namespace mrt {
+
+namespace {
+
+constexpr int kMaxDepth = 64;          // SplitBVHBuilder.hh:41-45
+constexpr int kMaxSpatialDepth = 48;
+constexpr int kNumSpatialBins = 128;
+constexpr int kParallelMinRefs = 8192; // subtrees at least this large may run on their own thread
+
+struct Ref {
+    int32_t triIdx = -1;
+    AABB bounds;
+};
+struct NodeSpec {
+    int numRef = 0;
+    AABB bounds;
+};
+struct ObjectSplit {
+    float sah = FLT_MAX;
+    int sortDim = 0;
+    int numLeft = 0;
+    AABB leftBounds, rightBounds;
+};
+struct SpatialSplit {
+    float sah = FLT_MAX;
+    int dim = 0;
+    float pos = 0.0f;
+};
+struct SpatialBin {
+    AABB bounds;
+    int enter = 0;
+    int exit = 0;
+};
+
+// (S32) of a float as x86-64 cvttss2si computes it: truncation, and the
+// "integer indefinite" 0x80000000 for NaN and out-of-range values.
+inline int trunc_to_int(float x) {
+    if (!(x >= -2147483648.0f && x < 2147483648.0f)) return INT_MIN;
+    return (int)x;
+}
+inline int clampi(int v, int lo, int hi) { return std::min(std::max(v, lo), hi); }
+
+// FW::sort over a Ref array ordered by (min+max)[dim], then triIdx
+// (SplitBVHBuilder.cc:75-84 with Sort.cc:63-239).
+class RefSorter {
+public:
+    RefSorter(std::vector<Ref>& r, int dim) : refs_(r), dim_(dim) {}
+
+    void sort(int start, int end) {
+        if (end - start < 2) return;
+        qsort(start, end);
+    }
+
+private:
+    bool less(int a, int b) const {
+        const Ref& ra = refs_[a];
+        const Ref& rb = refs_[b];
+        const float ca = ra.bounds.mn[dim_] + ra.bounds.mx[dim_];
+        const float cb = rb.bounds.mn[dim_] + rb.bounds.mx[dim_];
+        return ca < cb || (ca == cb && ra.triIdx < rb.triIdx);
+    }
+    void swp(int a, int b) { std::swap(refs_[a], refs_[b]); }
+
+    void insertion_sort(int start, int size) {
+        for (int i = 1; i < size; i++) {
+            int j = start + i - 1;
+            while (j >= start && less(j + 1, j)) {
+                swp(j, j + 1);
+                j--;
+            }
+        }
+    }
+    int median3(int low, int high) const {
+        int l = low;
+        int c = (low + high) >> 1;
+        int h = high - 2;
+        if (less(h, l)) std::swap(l, h);
+        if (less(c, l)) c = l;
+        return less(h, c) ? h : c;
+    }
+    int partition(int low, int high) {
+        swp(median3(low, high), high - 1);
+        int i = low - 1;
+        int j = high - 1;
+        for (;;) {
+            do i++; while (less(i, high - 1));
+            do j--; while (less(high - 1, j));
+            if (i >= j) break;
+            swp(i, j);
+        }
+        swp(i, high - 1);
+        return i;
+    }
+    void qsort(int low, int high) {
+        constexpr int kStack = 32, kMin = 16;
+        int stack[kStack];
+        int sp = 0;
+        stack[sp++] = high;
+        while (sp) {
+            high = stack[--sp];
+            if (high - low < kMin || sp + 2 > kStack) {
+                insertion_sort(low, high - low);
+                low = high + 1;
+                continue;
+            }
+            const int i = partition(low, high);
+            if (high - i > 2) stack[sp++] = high;
+            if (i - low > 1) stack[sp++] = i;
+            else low = i + 1;
+        }
+    }
+
+    std::vector<Ref>& refs_;
+    int dim_;
+};
+
+class Builder {
+public:
+    Builder(const Scene& s, const BuildParams& p) : sc_(s), p_(p) {
+        int threads = p.threads > 0 ? p.threads : (int)std::thread::hardware_concurrency();
+        freeThreads_.store(std::max(0, threads - 1));
+    }
+
+    std::unique_ptr<BvhNode> run() {   // SplitBVHBuilder.cc:55-100
+        NodeSpec root;
+        std::vector<Ref> refs(sc_.triangles.size());
+        for (size_t i = 0; i < refs.size(); i++) {
+            refs[i].triIdx = (int32_t)i;
+            const Vec3i& t = sc_.triangles[i];
+            for (int j = 0; j < 3; j++) refs[i].bounds.grow(sc_.vertices[t[j]]);
+            root.bounds.grow(refs[i].bounds);
+        }
+        root.numRef = (int)refs.size();
+        minOverlap_ = root.bounds.area() * p_.splitAlpha;
+        return build(std::move(refs), root, 0);
+    }
+
+private:
+    float tri_cost(int n) const {
+        return (float)(((n + p_.triBatchSize - 1) / p_.triBatchSize) * p_.triBatchSize) * p_.sahTriangleCost;
+    }
+    float node_cost(int n) const {
+        return (float)(((n + p_.nodeBatchSize - 1) / p_.nodeBatchSize) * p_.nodeBatchSize) * p_.sahNodeCost;
+    }
+
+    // SplitBVHBuilder.cc:113-174. `refs` is exactly the node's segment of the
+    // reference's m_refStack, in the same order.
+    std::unique_ptr<BvhNode> build(std::vector<Ref> refs, NodeSpec spec, int level) {
+        // Remove degenerates (:120-129).
+        for (int i = (int)refs.size() - 1; i >= 0; i--) {
+            const Vec3f size = refs[i].bounds.mx - refs[i].bounds.mn;
+            if (size.min_comp() < 0.0f || size.sum() == size.max_comp()) {
+                refs[i] = refs.back();
+                refs.pop_back();
+            }
+        }
+        spec.numRef = (int)refs.size();
+
+        if (spec.numRef <= p_.minLeafSize || level >= kMaxDepth) return make_leaf(refs, spec);
+
+        const float area = spec.bounds.area();
+        const float leafSAH = area * tri_cost(spec.numRef);
+        const float nodeSAH = area * node_cost(2);
+        const ObjectSplit object = find_object_split(refs, nodeSAH);
+
+        SpatialSplit spatial;
+        if (level < kMaxSpatialDepth) {
+            AABB overlap = object.leftBounds;
+            overlap.intersect(object.rightBounds);
+            if (overlap.area() >= minOverlap_) spatial = find_spatial_split(refs, spec, nodeSAH);
+        }
+
+        const float minSAH = fw_min(fw_min(leafSAH, object.sah), spatial.sah);
+        if (minSAH == leafSAH && spec.numRef <= p_.maxLeafSize) return make_leaf(refs, spec);
+
+        NodeSpec left, right;
+        if (minSAH == spatial.sah) perform_spatial_split(left, right, refs, spatial);
+        if (!left.numRef || !right.numRef) perform_object_split(left, right, refs, spec, object);
+
+        std::vector<Ref> rightRefs(refs.begin() + left.numRef, refs.end());
+        refs.resize(left.numRef);
+
+        auto node = std::make_unique<BvhNode>();
+        node->bounds = spec.bounds;
+        std::unique_ptr<BvhNode> rightNode;
+        std::thread worker;
+        if (right.numRef >= kParallelMinRefs && left.numRef >= kParallelMinRefs && take_thread()) {
+            worker = std::thread([&, lvl = level + 1] { rightNode = build(std::move(rightRefs), right, lvl); });
+        } else {
+            rightNode = build(std::move(rightRefs), right, level + 1);
+        }
+        std::unique_ptr<BvhNode> leftNode = build(std::move(refs), left, level + 1);
+        if (worker.joinable()) {
+            worker.join();
+            freeThreads_.fetch_add(1);
+        }
+        node->child[0] = std::move(leftNode);
+        node->child[1] = std::move(rightNode);
+        return node;
+    }
+
+    bool take_thread() {
+        int f = freeThreads_.load();
+        while (f > 0)
+            if (freeThreads_.compare_exchange_weak(f, f - 1)) return true;
+        return false;
+    }
+
+    // createLeaf (:178-187): triangles in m_refStack.removeLast() order.
+    std::unique_ptr<BvhNode> make_leaf(const std::vector<Ref>& refs, const NodeSpec& spec) {
+        auto leaf = std::make_unique<BvhNode>();
+        leaf->bounds = spec.bounds;
+        leaf->tris.reserve(refs.size());
+        for (int i = (int)refs.size() - 1; i >= 0; i--) leaf->tris.push_back(refs[i].triIdx);
+        return leaf;
+    }
+
+    // findObjectSplit (:191-231): three full sorts, right-to-left bound sweep.
+    ObjectSplit find_object_split(std::vector<Ref>& refs, float nodeSAH) const {
+        ObjectSplit split;
+        const int n = (int)refs.size();
+        float bestTieBreak = FLT_MAX;
+        std::vector<AABB> rightBounds(std::max(n - 1, 1));
+        for (int dim = 0; dim < 3; dim++) {
+            RefSorter(refs, dim).sort(0, n);
+            AABB rb;
+            for (int i = n - 1; i > 0; i--) {
+                rb.grow(refs[i].bounds);
+                rightBounds[i - 1] = rb;
+            }
+            AABB lb;
+            for (int i = 1; i < n; i++) {
+                lb.grow(refs[i - 1].bounds);
+                const float sah = nodeSAH + lb.area() * tri_cost(i) + rightBounds[i - 1].area() * tri_cost(n - i);
+                const float tieBreak = (float)i * (float)i + (float)(n - i) * (float)(n - i);
+                if (sah < split.sah || (sah == split.sah && tieBreak < bestTieBreak)) {
+                    split.sah = sah;
+                    split.sortDim = dim;
+                    split.numLeft = i;
+                    split.leftBounds = lb;
+                    split.rightBounds = rightBounds[i - 1];
+                    bestTieBreak = tieBreak;
+                }
+            }
+        }
+        return split;
+    }
+
+    // performObjectSplit (:235-245).
+    void perform_object_split(NodeSpec& left, NodeSpec& right, std::vector<Ref>& refs, const NodeSpec& spec,
+                              const ObjectSplit& split) const {
+        RefSorter(refs, split.sortDim).sort(0, (int)refs.size());
+        left.numRef = split.numLeft;
+        left.bounds = split.leftBounds;
+        right.numRef = spec.numRef - split.numLeft;
+        right.bounds = split.rightBounds;
+    }
+
+    // findSpatialSplit (:249-327).
+    SpatialSplit find_spatial_split(const std::vector<Ref>& refs, const NodeSpec& spec, float nodeSAH) const {
+        const Vec3f origin = spec.bounds.mn;
+        const Vec3f binSize = (spec.bounds.mx - origin) * (1.0f / (float)kNumSpatialBins);
+        const Vec3f invBinSize(1.0f / binSize.x, 1.0f / binSize.y, 1.0f / binSize.z);
+
+        std::vector<SpatialBin> bins(3 * kNumSpatialBins);
+        auto bin = [&](int dim, int i) -> SpatialBin& { return bins[dim * kNumSpatialBins + i]; };
+
+        for (const Ref& ref : refs) {
+            const Vec3f lo = (ref.bounds.mn - origin) * invBinSize;
+            const Vec3f hi = (ref.bounds.mx - origin) * invBinSize;
+            int firstBin[3], lastBin[3];
+            for (int d = 0; d < 3; d++) {
+                firstBin[d] = clampi(trunc_to_int(lo[d]), 0, kNumSpatialBins - 1);
+                lastBin[d] = clampi(trunc_to_int(hi[d]), firstBin[d], kNumSpatialBins - 1);
+            }
+            for (int dim = 0; dim < 3; dim++) {
+                Ref curr = ref;
+                for (int i = firstBin[dim]; i < lastBin[dim]; i++) {
+                    Ref l, r;
+                    split_reference(l, r, curr, dim, origin[dim] + binSize[dim] * (float)(i + 1));
+                    bin(dim, i).bounds.grow(l.bounds);
+                    curr = r;
+                }
+                bin(dim, lastBin[dim]).bounds.grow(curr.bounds);
+                bin(dim, firstBin[dim]).enter++;
+                bin(dim, lastBin[dim]).exit++;
+            }
+        }
+
+        SpatialSplit split;
+        AABB rightBounds[kNumSpatialBins - 1];
+        for (int dim = 0; dim < 3; dim++) {
+            AABB rb;
+            for (int i = kNumSpatialBins - 1; i > 0; i--) {
+                rb.grow(bin(dim, i).bounds);
+                rightBounds[i - 1] = rb;
+            }
+            AABB lb;
+            int leftNum = 0;
+            int rightNum = spec.numRef;
+            for (int i = 1; i < kNumSpatialBins; i++) {
+                lb.grow(bin(dim, i - 1).bounds);
+                leftNum += bin(dim, i - 1).enter;
+                rightNum -= bin(dim, i - 1).exit;
+                const float sah = nodeSAH + lb.area() * tri_cost(leftNum) + rightBounds[i - 1].area() * tri_cost(rightNum);
+                if (sah < split.sah) {
+                    split.sah = sah;
+                    split.dim = dim;
+                    split.pos = origin[dim] + binSize[dim] * (float)i;
+                }
+            }
+        }
+        return split;
+    }
+
+    // performSpatialSplit (:331-421).
+    void perform_spatial_split(NodeSpec& left, NodeSpec& right, std::vector<Ref>& refs, const SpatialSplit& split) const {
+        const int leftStart = 0;
+        int leftEnd = leftStart;
+        int rightStart = (int)refs.size();
+        left.bounds = right.bounds = AABB();
+
+        for (int i = leftEnd; i < rightStart; i++) {
+            if (refs[i].bounds.mx[split.dim] <= split.pos) {   // entirely left
+                left.bounds.grow(refs[i].bounds);
+                std::swap(refs[i], refs[leftEnd++]);
+            } else if (refs[i].bounds.mn[split.dim] >= split.pos) {   // entirely right
+                right.bounds.grow(refs[i].bounds);
+                std::swap(refs[i], refs[--rightStart]);
+                i--;
+            }
+        }
+
+        while (leftEnd < rightStart) {   // straddlers: duplicate or unsplit
+            Ref lref, rref;
+            split_reference(lref, rref, refs[leftEnd], split.dim, split.pos);
+
+            AABB lub = left.bounds, rub = right.bounds, ldb = left.bounds, rdb = right.bounds;
+            lub.grow(refs[leftEnd].bounds);
+            rub.grow(refs[leftEnd].bounds);
+            ldb.grow(lref.bounds);
+            rdb.grow(rref.bounds);
+
+            const int size = (int)refs.size();
+            const float lac = tri_cost(leftEnd - leftStart);
+            const float rac = tri_cost(size - rightStart);
+            const float lbc = tri_cost(leftEnd - leftStart + 1);
+            const float rbc = tri_cost(size - rightStart + 1);
+
+            const float unsplitLeftSAH = lub.area() * lbc + right.bounds.area() * rac;
+            const float unsplitRightSAH = left.bounds.area() * lac + rub.area() * rbc;
+            const float duplicateSAH = ldb.area() * lbc + rdb.area() * rbc;
+            const float minSAH = fw_min(fw_min(unsplitLeftSAH, unsplitRightSAH), duplicateSAH);
+
+            if (minSAH == unsplitLeftSAH) {
+                left.bounds = lub;
+                leftEnd++;
+            } else if (minSAH == unsplitRightSAH) {
+                right.bounds = rub;
+                std::swap(refs[leftEnd], refs[--rightStart]);
+            } else {
+                left.bounds = ldb;
+                right.bounds = rdb;
+                refs[leftEnd++] = lref;
+                refs.push_back(rref);
+            }
+        }
+        left.numRef = leftEnd - leftStart;
+        right.numRef = (int)refs.size() - rightStart;
+    }
+
+    // splitReference (:425-470).
+    void split_reference(Ref& left, Ref& right, const Ref& ref, int dim, float pos) const {
+        left.triIdx = right.triIdx = ref.triIdx;
+        left.bounds = right.bounds = AABB();
+        const Vec3i& inds = sc_.triangles[ref.triIdx];
+        const Vec3f* v1 = &sc_.vertices[inds.z];
+        for (int i = 0; i < 3; i++) {
+            const Vec3f* v0 = v1;
+            v1 = &sc_.vertices[inds[i]];
+            const float v0p = (*v0)[dim];
+            const float v1p = (*v1)[dim];
+            if (v0p <= pos) left.bounds.grow(*v0);
+            if (v0p >= pos) right.bounds.grow(*v0);
+            if ((v0p < pos && v1p > pos) || (v0p > pos && v1p < pos)) {
+                const float t = fw_min(fw_max((pos - v0p) / (v1p - v0p), 0.0f), 1.0f);
+                const float s = 1.0f - t;
+                const Vec3f p((*v0).x * s + (*v1).x * t, (*v0).y * s + (*v1).y * t, (*v0).z * s + (*v1).z * t);
+                left.bounds.grow(p);
+                right.bounds.grow(p);
+            }
+        }
+        left.bounds.mx[dim] = pos;
+        right.bounds.mn[dim] = pos;
+        left.bounds.intersect(ref.bounds);
+        right.bounds.intersect(ref.bounds);
+    }
+
+    const Scene& sc_;
+    const BuildParams& p_;
+    float minOverlap_ = 0.0f;
+    std::atomic<int> freeThreads_{0};
+};
+
+void collect_stats(const BvhNode& n, int depth, float rootArea, const BuildParams& p, BvhStats& s) {
+    s.maxDepth = std::max<int64_t>(s.maxDepth, depth);
+    const float prob = rootArea > 0.0f ? n.bounds.area() / rootArea : 0.0f;
+    if (n.is_leaf()) {
+        s.leafNodes++;
+        s.triRefs += (int64_t)n.tris.size();
+        s.sahCost += prob * (float)n.tris.size() * p.sahTriangleCost;
+        return;
+    }
+    s.innerNodes++;
+    s.sahCost += prob * 2.0f * p.sahNodeCost;
+    collect_stats(*n.child[0], depth + 1, rootArea, p, s);
+    collect_stats(*n.child[1], depth + 1, rootArea, p, s);
+}
+
+}  // namespace
+
+std::unique_ptr<BvhNode> build_sbvh(const Scene& scene, const BuildParams& params, BvhStats* stats) {
+    const auto t0 = std::chrono::steady_clock::now();
+    Builder b(scene, params);
+    std::unique_ptr<BvhNode> root = b.run();
+    if (stats) {
+        *stats = BvhStats();
+        collect_stats(*root, 0, root->bounds.area(), params, *stats);
+        stats->buildSeconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return root;
+}
+
+}  // namespace mrt

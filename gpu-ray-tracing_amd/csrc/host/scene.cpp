@@ -1,0 +1,452 @@
+// scene.cpp — Scene flattening + deterministic synthetic stand-ins.
+//
+// The README scenes (README.md:46-81) are not available here; each generator
+// builds geometry of the same character with the published triangle count
+// exactly: a displaced closed blob in open space (bunny), a
+// small displaced knob (Mori knob), a furnished closed room (conference), an
+// open-roof colonnaded atrium (sponza) and a ball of thin random-walk tubes
+// (hairball). Everything is derived from a splitmix64 stream and libm, so the
+// same binary produces bit-identical scenes on every host.
+#include "scene.hpp"
+
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstdio>
+#include <fstream>
+#include <functional>
+#include <sstream>
+
+namespace mrt {
+
+namespace {
+
+constexpr double kPi = 3.14159265358979323846;
+
+struct Rng {
+    uint64_t s;
+    explicit Rng(uint64_t seed) : s(seed * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull) {}
+    uint64_t next() {   // splitmix64
+        uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    }
+    double uniform() { return (double)(next() >> 11) * (1.0 / 9007199254740992.0); }
+    double range(double a, double b) { return a + (b - a) * uniform(); }
+};
+
+struct Mesher {
+    Scene& sc;
+    explicit Mesher(Scene& s) : sc(s) {}
+
+    int vert(double x, double y, double z) {
+        sc.vertices.emplace_back((float)x, (float)y, (float)z);
+        return (int)sc.vertices.size() - 1;
+    }
+    void tri(int a, int b, int c) { sc.triangles.push_back(Vec3i{a, b, c}); }
+    void quad(int a, int b, int c, int d) {   // a-b-c-d counter-clockwise
+        tri(a, b, c);
+        tri(a, c, d);
+    }
+
+    // Parametric patch p(u, v) on [0,1]^2 with nu x nv quads; wrapU closes the
+    // seam in u (cylinders, tori).
+    void grid(int nu, int nv, bool wrapU, bool wrapV, const std::function<void(double, double, double*)>& p) {
+        const int cu = wrapU ? nu : nu + 1;
+        const int cv = wrapV ? nv : nv + 1;
+        const int base = (int)sc.vertices.size();
+        for (int j = 0; j < cv; j++)
+            for (int i = 0; i < cu; i++) {
+                double q[3];
+                p((double)i / nu, (double)j / nv, q);
+                vert(q[0], q[1], q[2]);
+            }
+        for (int j = 0; j < nv; j++)
+            for (int i = 0; i < nu; i++) {
+                const int i1 = wrapU ? (i + 1) % nu : i + 1;
+                const int j1 = wrapV ? (j + 1) % nv : j + 1;
+                quad(base + j * cu + i, base + j * cu + i1, base + j1 * cu + i1, base + j1 * cu + i);
+            }
+    }
+
+    // Closed UV sphere-like surface r(theta, phi): 2 * nu * (nv - 1) triangles.
+    void blob(int nu, int nv, double cx, double cy, double cz, const std::function<double(double, double)>& radius,
+              double sx = 1, double sy = 1, double sz = 1) {
+        const int base = (int)sc.vertices.size();
+        auto pos = [&](double th, double ph) {
+            const double r = radius(th, ph);
+            return std::array<double, 3>{cx + sx * r * std::sin(th) * std::cos(ph), cy + sy * r * std::cos(th),
+                                         cz + sz * r * std::sin(th) * std::sin(ph)};
+        };
+        const auto top = pos(0.0, 0.0);
+        const int itop = vert(top[0], top[1], top[2]);
+        for (int j = 1; j < nv; j++)
+            for (int i = 0; i < nu; i++) {
+                const auto p = pos(kPi * j / nv, 2 * kPi * i / nu);
+                vert(p[0], p[1], p[2]);
+            }
+        const auto bot = pos(kPi, 0.0);
+        const int ibot = vert(bot[0], bot[1], bot[2]);
+        auto ring = [&](int j, int i) { return base + 1 + (j - 1) * nu + (i % nu); };
+        for (int i = 0; i < nu; i++) tri(itop, ring(1, i + 1), ring(1, i));
+        for (int j = 1; j < nv - 1; j++)
+            for (int i = 0; i < nu; i++) quad(ring(j, i), ring(j, i + 1), ring(j + 1, i + 1), ring(j + 1, i));
+        for (int i = 0; i < nu; i++) tri(ibot, ring(nv - 1, i), ring(nv - 1, i + 1));
+    }
+
+    // Axis-aligned box, every face split into n x n quads: 12 n^2 triangles.
+    void box(double x0, double y0, double z0, double x1, double y1, double z1, int n) {
+        auto face = [&](int axis, double c, bool flip) {
+            grid(n, n, false, false, [&](double u, double v, double* q) {
+                const double a = flip ? 1.0 - u : u;
+                if (axis == 0) { q[0] = c; q[1] = y0 + (y1 - y0) * a; q[2] = z0 + (z1 - z0) * v; }
+                if (axis == 1) { q[1] = c; q[2] = z0 + (z1 - z0) * a; q[0] = x0 + (x1 - x0) * v; }
+                if (axis == 2) { q[2] = c; q[0] = x0 + (x1 - x0) * a; q[1] = y0 + (y1 - y0) * v; }
+            });
+        };
+        face(0, x0, true); face(0, x1, false);
+        face(1, y0, true); face(1, y1, false);
+        face(2, z0, true); face(2, z1, false);
+    }
+
+    // Open cylinder along y: 2 * sides * rings triangles.
+    void cylinder(double cx, double cz, double y0, double y1, double r, int sides, int rings,
+                  const std::function<double(double, double)>& profile = nullptr) {
+        grid(sides, rings, true, false, [&](double u, double v, double* q) {
+            const double rr = profile ? r * profile(u, v) : r;
+            q[0] = cx + rr * std::cos(2 * kPi * u);
+            q[1] = y0 + (y1 - y0) * v;
+            q[2] = cz + rr * std::sin(2 * kPi * u);
+        });
+    }
+
+    // Tube of radius r along a polyline: 2 * sides * (points - 1) triangles.
+    void tube(const std::vector<std::array<double, 3>>& pts, double r, int sides) {
+        const int n = (int)pts.size();
+        const int base = (int)sc.vertices.size();
+        for (int k = 0; k < n; k++) {
+            const auto& p = pts[k];
+            const auto& a = pts[k == 0 ? 0 : k - 1];
+            const auto& b = pts[k == n - 1 ? n - 1 : k + 1];
+            double t[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+            double tl = std::sqrt(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
+            if (tl == 0) tl = 1;
+            for (double& c : t) c /= tl;
+            double ref[3] = {0, 1, 0};
+            if (std::fabs(t[1]) > 0.9) { ref[0] = 1; ref[1] = 0; }
+            double u[3] = {t[1] * ref[2] - t[2] * ref[1], t[2] * ref[0] - t[0] * ref[2], t[0] * ref[1] - t[1] * ref[0]};
+            const double ul = std::sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+            for (double& c : u) c /= ul;
+            const double w[3] = {t[1] * u[2] - t[2] * u[1], t[2] * u[0] - t[0] * u[2], t[0] * u[1] - t[1] * u[0]};
+            for (int s = 0; s < sides; s++) {
+                const double ang = 2 * kPi * s / sides;
+                const double c = std::cos(ang) * r, d = std::sin(ang) * r;
+                vert(p[0] + c * u[0] + d * w[0], p[1] + c * u[1] + d * w[1], p[2] + c * u[2] + d * w[2]);
+            }
+        }
+        for (int k = 0; k + 1 < n; k++)
+            for (int s = 0; s < sides; s++) {
+                const int s1 = (s + 1) % sides;
+                quad(base + k * sides + s, base + k * sides + s1, base + (k + 1) * sides + s1, base + (k + 1) * sides + s);
+            }
+    }
+
+    // Triangle strip of exactly `count` triangles along a ribbon (used to land
+    // every generator on its published triangle count).
+    void strip(int count, double x0, double y, double z0, double length, double width) {
+        if (count <= 0) return;
+        const int cols = (count + 2) / 2;
+        const int base = (int)sc.vertices.size();
+        for (int c = 0; c <= cols; c++) {
+            const double x = x0 + length * c / cols;
+            vert(x, y, z0);
+            vert(x, y, z0 + width);
+        }
+        int made = 0;
+        for (int c = 0; c < cols && made < count; c++) {
+            const int a = base + 2 * c, b = a + 1, d = a + 2, e = a + 3;
+            tri(a, d, b);
+            if (++made < count) {
+                tri(b, d, e);
+                ++made;
+            }
+        }
+    }
+};
+
+bool finish(Scene& sc, int64_t target, std::string* err) {
+    if (target > 0 && (int64_t)sc.triangles.size() != target) {
+        if (err) {
+            char buf[160];
+            std::snprintf(buf, sizeof buf, "generator '%s' produced %zu triangles, expected %lld", sc.name.c_str(),
+                          sc.triangles.size(), (long long)target);
+            *err = buf;
+        }
+        return false;
+    }
+    sc.compute_normals();
+    return true;
+}
+
+void pad_to(Mesher& m, int64_t target, double x0, double y, double z0, double length, double width) {
+    const int64_t have = (int64_t)m.sc.triangles.size();
+    if (target > have) m.strip((int)(target - have), x0, y, z0, length, width);
+}
+
+Camera look_at(Vec3f pos, Vec3f target, Vec3f up, float fov, float nearD, float farD) {
+    Camera c;
+    c.position = pos;
+    c.forward = normalize(target - pos);
+    c.up = up;
+    c.fov = fov;
+    c.nearDist = nearD;
+    c.farDist = farD;
+    return c;
+}
+
+// ---- the README stand-ins ----------------------------------------------------
+
+void gen_bunny(Scene& sc, uint64_t seed) {   // 144 500 triangles
+    Mesher m(sc);
+    Rng rng(seed);
+    double ph[6];
+    for (double& p : ph) p = rng.range(0, 2 * kPi);
+    m.blob(250, 290, 0.0, 0.0, 0.0, [&](double th, double phi) {
+        return 1.0 + 0.10 * std::sin(3 * th + ph[0]) * std::sin(4 * phi + ph[1]) +
+               0.05 * std::sin(7 * th + ph[2]) * std::cos(5 * phi + ph[3]) +
+               0.02 * std::sin(17 * th + ph[4]) * std::sin(13 * phi + ph[5]);
+    }, 1.0, 0.85, 1.15);
+    sc.camera = look_at(Vec3f(0.3f, 0.45f, 3.6f), Vec3f(0.f, 0.f, 0.f), Vec3f(0.f, 1.f, 0.f), 45.f, 0.01f, 500.f);
+    sc.aoRadius = 5.0f;
+}
+
+void gen_mori(Scene& sc, uint64_t seed) {   // 12 570 triangles
+    Mesher m(sc);
+    Rng rng(seed);
+    const double p0 = rng.range(0, 2 * kPi);
+    m.blob(48, 48, 0.0, 1.6, 0.0, [&](double th, double phi) { return 0.55 + 0.04 * std::sin(6 * phi + p0) * std::sin(th); });
+    m.grid(64, 24, true, true, [&](double u, double v, double* q) {   // ring around the knob
+        const double R = 0.75, r = 0.08, a = 2 * kPi * u, b = 2 * kPi * v;
+        q[0] = (R + r * std::cos(b)) * std::cos(a);
+        q[1] = 1.25 + r * std::sin(b);
+        q[2] = (R + r * std::cos(b)) * std::sin(a);
+    });
+    m.cylinder(0.0, 0.0, 0.0, 1.2, 0.25, 48, 16, [](double, double v) { return 1.0 + 0.3 * (1.0 - v) * (1.0 - v); });
+    m.box(-1.2, -0.1, -1.2, 1.2, 0.0, 1.2, 6);   // 432
+    pad_to(m, 12570, -1.5, -0.1001, 1.3, 3.0, 0.2);
+    sc.camera = look_at(Vec3f(2.6f, 2.4f, 3.4f), Vec3f(0.f, 1.0f, 0.f), Vec3f(0.f, 1.f, 0.f), 45.f, 0.01f, 500.f);
+    sc.aoRadius = 5.0f;
+}
+
+void gen_conference(Scene& sc, uint64_t seed) {   // 350 949 triangles
+    Mesher m(sc);
+    Rng rng(seed);
+    const double W = 30.0, H = 8.0, D = 20.0;
+    const int n = 7;   // box face subdivision: 588 triangles per box
+    auto table = [&](double x, double z, double w, double d) {
+        m.box(x - w / 2, 0.95, z - d / 2, x + w / 2, 1.05, z + d / 2, n);
+        const double lx = w / 2 - 0.15, lz = d / 2 - 0.15;
+        for (int sx = -1; sx <= 1; sx += 2)
+            for (int sz = -1; sz <= 1; sz += 2)
+                m.box(x + sx * lx - 0.06, 0.0, z + sz * lz - 0.06, x + sx * lx + 0.06, 0.95, z + sz * lz + 0.06, n);
+    };
+    auto chair = [&](double x, double z, int facing) {   // facing: 0 +z, 1 -z, 2 +x, 3 -x
+        const double s = 0.5, jit = rng.range(-0.06, 0.06);
+        x += jit;
+        m.box(x - s / 2, 0.5, z - s / 2, x + s / 2, 0.58, z + s / 2, n);
+        const double bx = (facing == 2) ? -s / 2 : (facing == 3) ? s / 2 - 0.06 : -s / 2;
+        const double bz = (facing == 0) ? -s / 2 : (facing == 1) ? s / 2 - 0.06 : -s / 2;
+        if (facing < 2) m.box(x - s / 2, 0.58, z + bz, x + s / 2, 1.3, z + bz + 0.06, n);
+        else m.box(x + bx, 0.58, z - s / 2, x + bx + 0.06, 1.3, z + s / 2, n);
+        for (int sx = -1; sx <= 1; sx += 2)
+            for (int sz = -1; sz <= 1; sz += 2)
+                m.box(x + sx * 0.2 - 0.03, 0.0, z + sz * 0.2 - 0.03, x + sx * 0.2 + 0.03, 0.5, z + sz * 0.2 + 0.03, n);
+    };
+    // Central conference table with chairs on both long sides and the ends.
+    table(W / 2, D / 2, 12.0, 4.0);
+    for (int i = 0; i < 12; i++) {
+        const double x = W / 2 - 5.5 + i * 1.0;
+        chair(x, D / 2 - 2.6, 0);
+        chair(x, D / 2 + 2.6, 1);
+    }
+    chair(W / 2 - 6.8, D / 2, 2);
+    chair(W / 2 + 6.8, D / 2, 3);
+    // Side tables, four chairs each.
+    for (int r = 0; r < 2; r++)
+        for (int c = 0; c < 6; c++) {
+            const double x = 3.0 + c * 4.8, z = (r == 0) ? 2.6 : D - 2.6;
+            table(x, z, 1.6, 1.2);
+            chair(x - 0.5, z - 1.1, 0);
+            chair(x + 0.5, z - 1.1, 0);
+            chair(x - 0.5, z + 1.1, 1);
+            chair(x + 0.5, z + 1.1, 1);
+        }
+    // Ceiling lamps: shaded cylinders.
+    for (int i = 0; i < 24; i++) {
+        const double x = 2.5 + (i % 6) * 5.0, z = 3.0 + (i / 6) * 4.7;
+        m.cylinder(x, z, H - 1.2, H - 0.6, 0.45, 32, 10, [](double, double v) { return 1.0 - 0.5 * v; });
+    }
+    // Room shell (inward facing): floor, ceiling, walls; resolution fills most of the budget.
+    const int64_t target = 350949;
+    const int64_t remaining = target - (int64_t)sc.triangles.size();
+    const int wallRes = std::max(8, (int)std::sqrt((double)remaining / (2.0 * 6.0)) - 2);
+    m.grid(wallRes, wallRes, false, false, [&](double u, double v, double* q) { q[0] = W * u; q[1] = 0; q[2] = D * v; });
+    m.grid(wallRes, wallRes, false, false, [&](double u, double v, double* q) { q[0] = W * v; q[1] = H; q[2] = D * u; });
+    m.grid(wallRes, wallRes, false, false, [&](double u, double v, double* q) { q[0] = W * v; q[1] = H * u; q[2] = 0; });
+    m.grid(wallRes, wallRes, false, false, [&](double u, double v, double* q) { q[0] = W * u; q[1] = H * v; q[2] = D; });
+    m.grid(wallRes, wallRes, false, false, [&](double u, double v, double* q) { q[0] = 0; q[1] = H * v; q[2] = D * u; });
+    m.grid(wallRes, wallRes, false, false, [&](double u, double v, double* q) { q[0] = W; q[1] = H * u; q[2] = D * v; });
+    pad_to(m, target, 0.5, 0.001, 0.2, W - 1.0, 0.3);
+    sc.camera = look_at(Vec3f(1.5f, 4.2f, 1.5f), Vec3f(15.f, 1.0f, 10.f), Vec3f(0.f, 1.f, 0.f), 60.f, 0.05f, 100.f);
+    sc.aoRadius = 5.0f;
+}
+
+void gen_sponza(Scene& sc, uint64_t seed) {   // 121 384 triangles
+    Mesher m(sc);
+    Rng rng(seed);
+    const double L = 30.0, Wd = 12.0;   // atrium x in [-L/2, L/2], z in [-Wd/2, Wd/2]
+    // Two storeys of colonnades on both long sides.
+    for (int storey = 0; storey < 2; storey++) {
+        const double y0 = storey * 6.0, h = storey == 0 ? 4.5 : 3.5, r = storey == 0 ? 0.35 : 0.25;
+        for (int side = -1; side <= 1; side += 2)
+            for (int c = 0; c < 10; c++) {
+                const double x = -L / 2 + 1.5 + c * 3.0, z = side * (Wd / 2 - 1.0);
+                m.cylinder(x, z, y0 + 0.3, y0 + h, r, 24, 20, [](double u, double v) { return 1.0 + 0.04 * std::cos(24 * 2 * kPi * u) - 0.08 * v; });
+                m.box(x - r - 0.1, y0, z - r - 0.1, x + r + 0.1, y0 + 0.3, z + r + 0.1, 1);       // base
+                m.box(x - r - 0.15, y0 + h, z - r - 0.15, x + r + 0.15, y0 + h + 0.25, z + r + 0.15, 1);   // capital
+                if (c < 9) {   // arch to the next column
+                    std::vector<std::array<double, 3>> arc;
+                    for (int k = 0; k <= 16; k++) {
+                        const double a = kPi * k / 16;
+                        arc.push_back({x + 1.5 - 1.5 * std::cos(a), y0 + h + 0.25 + 1.2 * std::sin(a), z});
+                    }
+                    m.tube(arc, 0.18, 12);
+                }
+            }
+        // Gallery floor slab over the ground colonnade.
+        if (storey == 0)
+            for (int side = -1; side <= 1; side += 2)
+                m.box(-L / 2, 5.9, side > 0 ? Wd / 2 - 1.6 : -Wd / 2, L / 2, 6.0, side > 0 ? Wd / 2 : -Wd / 2 + 1.6, 6);
+    }
+    // Hanging curtains (displaced sheets) between upper columns.
+    for (int k = 0; k < 6; k++) {
+        const double x0 = -L / 2 + 3.0 + k * 4.5, side = (k % 2) ? 1.0 : -1.0, p = rng.range(0, 2 * kPi);
+        m.grid(40, 30, false, false, [&](double u, double v, double* q) {
+            q[0] = x0 + 2.4 * u;
+            q[1] = 9.4 - 4.0 * v;
+            q[2] = side * (Wd / 2 - 1.3) + 0.25 * std::sin(6 * kPi * u + p) * v;
+        });
+    }
+    // Floor, outer walls, end walls; open roof. Tessellation fills the budget.
+    const int64_t target = 121384;
+    const int64_t remaining = target - (int64_t)sc.triangles.size();
+    const int res = std::max(8, (int)std::sqrt((double)remaining / (2.0 * 5.0)) - 2);
+    m.grid(res, res, false, false, [&](double u, double v, double* q) { q[0] = -L / 2 + L * u; q[1] = 0; q[2] = -Wd / 2 + Wd * v; });
+    for (int side = -1; side <= 1; side += 2)
+        m.grid(res, res, false, false, [&](double u, double v, double* q) {
+            q[0] = -L / 2 + L * u; q[1] = 12.0 * v; q[2] = side * Wd / 2 + 0.03 * std::sin(40 * u) * std::sin(30 * v);
+        });
+    for (int end = -1; end <= 1; end += 2)
+        m.grid(res, res, false, false, [&](double u, double v, double* q) { q[0] = end * L / 2; q[1] = 12.0 * v; q[2] = -Wd / 2 + Wd * u; });
+    pad_to(m, target, -L / 2 + 0.5, 0.001, -0.2, L - 1.0, 0.4);
+    sc.camera = look_at(Vec3f(-13.5f, 2.2f, 0.4f), Vec3f(10.f, 4.5f, -0.3f), Vec3f(0.f, 1.f, 0.f), 60.f, 0.05f, 100.f);
+    sc.aoRadius = 5.0f;
+}
+
+void gen_hairball(Scene& sc, uint64_t seed) {   // 6 469 561 triangles
+    Mesher m(sc);
+    Rng rng(seed);
+    const int tubes = 29950, segments = 18, sides = 6;
+    sc.vertices.reserve((size_t)tubes * (segments + 1) * sides + 4096);
+    sc.triangles.reserve(6469561);
+    std::vector<std::array<double, 3>> pts(segments + 1);
+    for (int t = 0; t < tubes; t++) {
+        // Start uniformly inside the unit ball, random-walk with momentum, pulled back at the rim.
+        double p[3], d[3];
+        do {
+            for (double& c : p) c = rng.range(-1, 1);
+        } while (p[0] * p[0] + p[1] * p[1] + p[2] * p[2] > 1.0);
+        for (double& c : d) c = rng.range(-1, 1);
+        for (int k = 0; k <= segments; k++) {
+            pts[k] = {p[0], p[1], p[2]};
+            for (int c = 0; c < 3; c++) d[c] = 0.75 * d[c] + 0.5 * rng.range(-1, 1);
+            const double r2 = p[0] * p[0] + p[1] * p[1] + p[2] * p[2];
+            if (r2 > 0.8)
+                for (int c = 0; c < 3; c++) d[c] -= 0.6 * p[c];
+            const double dl = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]) + 1e-12;
+            for (int c = 0; c < 3; c++) p[c] += 0.035 * d[c] / dl;
+        }
+        m.tube(pts, 0.0035, sides);
+    }
+    pad_to(m, 6469561, -0.2, -1.2, -0.2, 0.4, 0.05);
+    sc.camera = look_at(Vec3f(0.35f, 0.6f, 2.3f), Vec3f(0.f, 0.f, 0.f), Vec3f(0.f, 1.f, 0.f), 50.f, 0.01f, 100.f);
+    sc.aoRadius = 0.1f;
+}
+
+void gen_sphere(Scene& sc, int64_t param) {
+    Mesher m(sc);
+    const int n = (int)std::max<int64_t>(4, param);
+    m.blob(2 * n, n, 0.0, 0.0, 0.0, [](double, double) { return 1.0; });
+    sc.camera = look_at(Vec3f(0.f, 0.f, 3.5f), Vec3f(0.f, 0.f, 0.f), Vec3f(0.f, 1.f, 0.f), 45.f, 0.01f, 500.f);
+}
+
+void gen_random(Scene& sc, int64_t count, uint64_t seed) {   // uniformly scattered small triangles
+    Mesher m(sc);
+    Rng rng(seed);
+    for (int64_t i = 0; i < count; i++) {
+        const double cx = rng.range(-1, 1), cy = rng.range(-1, 1), cz = rng.range(-1, 1);
+        const double s = rng.range(0.02, 0.15);
+        const int a = m.vert(cx + s * rng.range(-1, 1), cy + s * rng.range(-1, 1), cz + s * rng.range(-1, 1));
+        const int b = m.vert(cx + s * rng.range(-1, 1), cy + s * rng.range(-1, 1), cz + s * rng.range(-1, 1));
+        const int c = m.vert(cx + s * rng.range(-1, 1), cy + s * rng.range(-1, 1), cz + s * rng.range(-1, 1));
+        m.tri(a, b, c);
+    }
+    sc.camera = look_at(Vec3f(0.f, 0.2f, 3.2f), Vec3f(0.f, 0.f, 0.f), Vec3f(0.f, 1.f, 0.f), 50.f, 0.01f, 100.f);
+    sc.aoRadius = 0.5f;
+}
+
+}  // namespace
+
+void Scene::compute_normals() {   // Scene.cc:66-75
+    triNormals.resize(triangles.size());
+    for (size_t i = 0; i < triangles.size(); i++) {
+        const Vec3i& t = triangles[i];
+        triNormals[i] = normalize(cross(vertices[t.y] - vertices[t.x], vertices[t.z] - vertices[t.x]));
+    }
+}
+
+AABB Scene::bounds() const {
+    AABB b;
+    for (const Vec3f& v : vertices) b.grow(v);
+    return b;
+}
+
+int64_t published_triangle_count(const std::string& name) {
+    if (name == "mori") return 12570;
+    if (name == "bunny") return 144500;
+    if (name == "conference") return 350949;
+    if (name == "sponza") return 121384;
+    if (name == "hairball") return 6469561;
+    if (name == "dragon") return 910348;
+    return -1;
+}
+
+bool make_synthetic_scene(const std::string& name, int64_t param, uint64_t seed, Scene& out, std::string* err) {
+    out = Scene();
+    out.name = name;
+    if (name == "bunny") gen_bunny(out, seed);
+    else if (name == "mori") gen_mori(out, seed);
+    else if (name == "conference") gen_conference(out, seed);
+    else if (name == "sponza") gen_sponza(out, seed);
+    else if (name == "hairball") gen_hairball(out, seed);
+    else if (name == "sphere") gen_sphere(out, param);
+    else if (name == "random") gen_random(out, std::max<int64_t>(1, param), seed);
+    else {
+        if (err) *err = "unknown synthetic scene '" + name + "'";
+        return false;
+    }
+    return finish(out, published_triangle_count(name), err);
+}
+
+}  // namespace mrt

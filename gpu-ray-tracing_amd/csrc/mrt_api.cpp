@@ -1,0 +1,388 @@
+// mrt_api.cpp — the C-ABI of include/mrt.h: per-device tracer contexts, the
+// persistent-grid sizing, the workspace (queue heads, stack spill slab) and
+// the reference-compatible entry points of CudaTracerKernels.hh:42-52.
+//
+// The library never owns the caller's BVH/ray/result buffers (reference
+// ownership: CudaBVH.cc:101-109, RayBuffer.cc:42-81). It owns only its
+// workspace, sized for the persistent grid it launches.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "../../include/mrt.h"
+#include "trace_kernel.hpp"
+
+struct mrt_tracer {
+    int device = 0;
+    int numCUs = 0;
+    std::mutex mu;
+
+    // Bound Compact2 BVH (borrowed device pointers).
+    bool bound = false;
+    const void* nodes = nullptr;
+    int64_t nodeBytes = 0;
+    const void* woop = nullptr;
+    int64_t woopBytes = 0;
+    const int32_t* triIndex = nullptr;
+    int64_t triIndexBytes = 0;
+
+    mrt_launch_cfg cfg{};
+
+    // Workspace.
+    unsigned* queues = nullptr;   // kMaxQueues * kQueueStrideWords words
+    int* status = nullptr;        // overflow counter
+    int* spill = nullptr;
+    size_t spillInts = 0;
+    hipEvent_t evStart = nullptr, evStop = nullptr;
+};
+
+namespace {
+
+thread_local std::string g_lastError;
+
+int fail(int code, const std::string& what) {
+    g_lastError = what;
+    return code;
+}
+
+int hipFail(hipError_t e, const char* what) {
+    return fail(MRT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define MRT_HIP(call)                                  \
+    do {                                               \
+        hipError_t e_ = (call);                        \
+        if (e_ != hipSuccess) return hipFail(e_, #call); \
+    } while (0)
+
+// Restores the caller's current device on scope exit.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+mrt_launch_cfg default_cfg() {
+    mrt_launch_cfg c;
+    c.waves_per_cu = 32;
+    c.fetch_threshold = 40;
+    c.num_queues = 8;
+    c.lds_stack = 16;
+    return c;
+}
+
+bool valid_cfg(const mrt_launch_cfg& c) {
+    return c.waves_per_cu >= 4 && c.waves_per_cu <= 32 && c.fetch_threshold >= 0 && c.fetch_threshold <= 64 &&
+           c.num_queues >= 1 && c.num_queues <= mrt::kMaxQueues &&
+           (c.lds_stack == 8 || c.lds_stack == 16 || c.lds_stack == 32);
+}
+
+mrt::TraceVariant variant_for(const mrt_tracer* t, uint32_t flags) {
+    mrt::TraceVariant v;
+    v.anyHit = (flags & MRT_TRACE_ANY_HIT) != 0;
+    v.exactRcp = (flags & MRT_TRACE_EXACT_RCP) != 0;
+    v.speculative = (flags & MRT_TRACE_LOCKSTEP_OFF) == 0;
+    v.stats = (flags & MRT_TRACE_STATS) != 0;
+    v.ldsStack = t->cfg.lds_stack;
+    return v;
+}
+
+// Persistent grid: as many 256-thread workgroups per CU as the config asks for
+// and the code object's occupancy admits; every workgroup is resident at once.
+int grid_blocks(const mrt_tracer* t, const mrt::TraceVariant& v, int* outBlocksPerCU) {
+    int occ = 0;
+    if (mrt::trace_occupancy(v, &occ) != hipSuccess || occ <= 0) occ = 1;
+    const int want = std::max(1, t->cfg.waves_per_cu / (mrt::kBlockThreads / 64));
+    const int perCU = std::min(want, occ);
+    if (outBlocksPerCU) *outBlocksPerCU = perCU;
+    return perCU * t->numCUs;
+}
+
+int ensure_workspace(mrt_tracer* t, int totalLanes, int ldsStack) {
+    if (!t->queues) {
+        MRT_HIP(hipMalloc(&t->queues, mrt::kMaxQueues * mrt::kQueueStrideWords * sizeof(unsigned)));
+        MRT_HIP(hipMalloc(&t->status, 64 * sizeof(int)));
+        MRT_HIP(hipMemset(t->status, 0, 64 * sizeof(int)));
+    }
+    const size_t need = (size_t)(mrt::kStackCapacity - ldsStack) * (size_t)totalLanes;
+    if (need > t->spillInts) {
+        if (t->spill) MRT_HIP(hipFree(t->spill));
+        t->spill = nullptr;
+        t->spillInts = 0;
+        MRT_HIP(hipMalloc(&t->spill, need * sizeof(int)));
+        t->spillInts = need;
+    }
+    if (!t->evStart) {
+        MRT_HIP(hipEventCreate(&t->evStart));
+        MRT_HIP(hipEventCreate(&t->evStop));
+    }
+    return MRT_OK;
+}
+
+int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, uint32_t flags, int32_t* stats,
+               void* stream, mrt_trace_info* info) {
+    if (!t) return fail(MRT_ERR_INVALID_ARG, "null tracer");
+    if (numRays < 0) return fail(MRT_ERR_INVALID_ARG, "numRays < 0");
+    if (flags & ~0xFu) return fail(MRT_ERR_INVALID_ARG, "unknown trace flag");
+    std::lock_guard<std::mutex> lock(t->mu);
+    if (info) std::memset(info, 0, sizeof(*info));
+    if (numRays == 0) return MRT_OK;   // reference CudaTracer.cc:123-125: no rays => 0 ms
+    if (!t->bound) return fail(MRT_ERR_NOT_BOUND, "trace before bind (no BVH)");
+    if (!rays || !results) return fail(MRT_ERR_INVALID_ARG, "null ray/result buffer");
+    if ((flags & MRT_TRACE_STATS) && !stats) return fail(MRT_ERR_INVALID_ARG, "MRT_TRACE_STATS without stats buffer");
+
+    DeviceGuard guard(t->device);
+    const mrt::TraceVariant v = variant_for(t, flags);
+    int perCU = 0;
+    const int blocks = grid_blocks(t, v, &perCU);
+    const int totalLanes = blocks * mrt::kBlockThreads;
+    if (int rc = ensure_workspace(t, totalLanes, v.ldsStack)) return rc;
+
+    mrt::TraceArgs a{};
+    a.rays = static_cast<const float4*>(rays);
+    a.results = static_cast<int2*>(results);
+    a.nodes = static_cast<const float4*>(t->nodes);
+    a.woop = static_cast<const float4*>(t->woop);
+    a.triIndex = t->triIndex;
+    a.nodeBytes = (uint32_t)t->nodeBytes;
+    a.woopBytes = (uint32_t)t->woopBytes;
+    a.numRays = numRays;
+    a.numQueues = std::min(t->cfg.num_queues, std::max(1, numRays));
+    a.fetchThreshold = t->cfg.fetch_threshold;
+    a.totalLanes = totalLanes;
+    a.queues = t->queues;
+    a.spill = t->spill;
+    a.status = t->status;
+    a.stats = reinterpret_cast<int4*>(stats);
+
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    MRT_HIP(hipMemsetAsync(t->queues, 0, mrt::kMaxQueues * mrt::kQueueStrideWords * sizeof(unsigned), s));
+    if (info) MRT_HIP(hipEventRecord(t->evStart, s));
+    MRT_HIP(mrt::launch_trace(v, a, blocks, s));
+    if (info) {
+        MRT_HIP(hipEventRecord(t->evStop, s));
+        MRT_HIP(hipEventSynchronize(t->evStop));
+        MRT_HIP(hipEventElapsedTime(&info->kernel_ms, t->evStart, t->evStop));
+        info->grid_waves = totalLanes / 64;
+        info->block_threads = mrt::kBlockThreads;
+        info->lds_stack_entries = v.ldsStack;
+        int overflow = 0;
+        MRT_HIP(hipMemcpy(&overflow, t->status, sizeof(int), hipMemcpyDeviceToHost));
+        info->stack_overflows = overflow;
+    }
+    return MRT_OK;
+}
+
+// ---- implicit per-device tracers (convenience + reference-compat API) ----
+constexpr int kMaxDevices = 64;
+std::mutex g_devMu;
+mrt_tracer* g_devTracer[kMaxDevices] = {};
+
+mrt_tracer* device_tracer(int* err) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) {
+        *err = fail(MRT_ERR_NO_DEVICE, "no current HIP device");
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> lock(g_devMu);
+    if (!g_devTracer[dev]) {
+        mrt_tracer* t = nullptr;
+        *err = mrt_tracer_create(dev, &t);
+        if (*err) return nullptr;
+        g_devTracer[dev] = t;
+    }
+    *err = MRT_OK;
+    return g_devTracer[dev];
+}
+
+// cutilSafeCall-style fatal error for the compat entry points
+// (reference cutil_inline_runtime.h:32-42).
+void compat_check(int rc, const char* file, int line) {
+    if (rc != MRT_OK) {
+        std::fprintf(stderr, "[%s,%d] (HIP error %d: %s)\n", file, line, rc, mrt_last_error_detail());
+        std::exit(-1);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int mrt_version(void) { return 100; }
+
+const char* mrt_error_string(int err) {
+    switch (err) {
+        case MRT_OK: return "ok";
+        case MRT_ERR_INVALID_ARG: return "invalid argument";
+        case MRT_ERR_NOT_BOUND: return "no BVH bound";
+        case MRT_ERR_HIP: return "HIP runtime error";
+        case MRT_ERR_NO_DEVICE: return "no HIP device";
+        case MRT_ERR_TOO_LARGE: return "buffer larger than 4 GiB";
+        default: return "unknown error";
+    }
+}
+
+const char* mrt_last_error_detail(void) { return g_lastError.c_str(); }
+
+int mrt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int mrt_tracer_create(int device, mrt_tracer** out) {
+    if (!out) return fail(MRT_ERR_INVALID_ARG, "null out");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(MRT_ERR_NO_DEVICE, "no HIP device visible");
+    if (device < 0 || device >= n) return fail(MRT_ERR_INVALID_ARG, "device index out of range");
+    int cus = 0;
+    MRT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    mrt_tracer* t = new mrt_tracer();
+    t->device = device;
+    t->numCUs = cus;
+    t->cfg = default_cfg();
+    *out = t;
+    return MRT_OK;
+}
+
+int mrt_tracer_destroy(mrt_tracer* t) {
+    if (!t) return MRT_OK;
+    {
+        DeviceGuard guard(t->device);
+        if (t->queues) (void)hipFree(t->queues);
+        if (t->status) (void)hipFree(t->status);
+        if (t->spill) (void)hipFree(t->spill);
+        if (t->evStart) (void)hipEventDestroy(t->evStart);
+        if (t->evStop) (void)hipEventDestroy(t->evStop);
+    }
+    delete t;
+    return MRT_OK;
+}
+
+int mrt_tracer_bind(mrt_tracer* t, const void* nodes, int64_t nodeBytes, const void* woop, int64_t woopBytes,
+                    const int32_t* triIndex, int64_t triIndexBytes) {
+    if (!t || !nodes || !woop || !triIndex) return fail(MRT_ERR_INVALID_ARG, "null BVH buffer");
+    if (nodeBytes < 64 || woopBytes < 16 || triIndexBytes < 4 || (nodeBytes % 64) || (woopBytes % 16) ||
+        (triIndexBytes % 4))
+        return fail(MRT_ERR_INVALID_ARG, "BVH buffer sizes are not Compact2-shaped");
+    if (nodeBytes > 0xFFFFFFF0ll || woopBytes > 0xFFFFFFF0ll)
+        return fail(MRT_ERR_TOO_LARGE, "Compact2 buffer above the 32-bit buffer-offset range");
+    if (triIndexBytes / 4 != woopBytes / 16) return fail(MRT_ERR_INVALID_ARG, "triIndex must hold one int per woop float4");
+    std::lock_guard<std::mutex> lock(t->mu);
+    t->nodes = nodes;
+    t->nodeBytes = nodeBytes;
+    t->woop = woop;
+    t->woopBytes = woopBytes;
+    t->triIndex = triIndex;
+    t->triIndexBytes = triIndexBytes;
+    t->bound = true;
+    return MRT_OK;
+}
+
+int mrt_tracer_unbind(mrt_tracer* t) {
+    if (!t) return fail(MRT_ERR_INVALID_ARG, "null tracer");
+    std::lock_guard<std::mutex> lock(t->mu);
+    t->bound = false;
+    t->nodes = t->woop = nullptr;
+    t->triIndex = nullptr;
+    return MRT_OK;
+}
+
+int mrt_tracer_set_config(mrt_tracer* t, const mrt_launch_cfg* cfg) {
+    if (!t || !cfg) return fail(MRT_ERR_INVALID_ARG, "null argument");
+    mrt_launch_cfg c = *cfg;
+    const mrt_launch_cfg d = default_cfg();
+    if (c.waves_per_cu == 0) c.waves_per_cu = d.waves_per_cu;
+    if (c.num_queues == 0) c.num_queues = d.num_queues;
+    if (c.lds_stack == 0) c.lds_stack = d.lds_stack;
+    if (!valid_cfg(c)) return fail(MRT_ERR_INVALID_ARG, "launch config out of range");
+    std::lock_guard<std::mutex> lock(t->mu);
+    t->cfg = c;
+    return MRT_OK;
+}
+
+int mrt_tracer_get_config(const mrt_tracer* t, mrt_launch_cfg* cfg) {
+    if (!t || !cfg) return fail(MRT_ERR_INVALID_ARG, "null argument");
+    *cfg = t->cfg;
+    return MRT_OK;
+}
+
+int mrt_tracer_trace(mrt_tracer* t, const void* rays, void* results, int32_t numRays, uint32_t flags,
+                     int32_t* stats, void* stream) {
+    return trace_impl(t, rays, results, numRays, flags, stats, stream, nullptr);
+}
+
+int mrt_tracer_trace_timed(mrt_tracer* t, const void* rays, void* results, int32_t numRays, uint32_t flags,
+                           int32_t* stats, void* stream, mrt_trace_info* info) {
+    mrt_trace_info local;
+    return trace_impl(t, rays, results, numRays, flags, stats, stream, info ? info : &local);
+}
+
+int mrt_bind_bvh(const void* nodes, int64_t nodeBytes, const void* woop, int64_t woopBytes,
+                 const int32_t* triIndex, int64_t triIndexBytes) {
+    int err = 0;
+    mrt_tracer* t = device_tracer(&err);
+    if (!t) return err;
+    return mrt_tracer_bind(t, nodes, nodeBytes, woop, woopBytes, triIndex, triIndexBytes);
+}
+
+int mrt_unbind_bvh(void) {
+    int err = 0;
+    mrt_tracer* t = device_tracer(&err);
+    if (!t) return err;
+    return mrt_tracer_unbind(t);
+}
+
+int mrt_trace(const void* rays, void* results, int32_t numRays, int32_t anyHit, void* stream, float* outMs) {
+    int err = 0;
+    mrt_tracer* t = device_tracer(&err);
+    if (!t) return err;
+    const uint32_t flags = anyHit ? MRT_TRACE_ANY_HIT : 0u;
+    if (!outMs) return trace_impl(t, rays, results, numRays, flags, nullptr, stream, nullptr);
+    mrt_trace_info info;
+    const int rc = trace_impl(t, rays, results, numRays, flags, nullptr, stream, &info);
+    *outMs = info.kernel_ms;
+    return rc;
+}
+
+// ---- reference-compatible entry points --------------------------------------
+
+void bind_CudaBVHTexture(void* nodeBuf, int64_t nodeBufSize, void* triWoopBuf, int64_t triWoopSize,
+                         int32_t* triIndexBuf, int64_t triIndexSize) {
+    compat_check(mrt_bind_bvh(nodeBuf, nodeBufSize, triWoopBuf, triWoopSize, triIndexBuf, triIndexSize), __FILE__,
+                 __LINE__);
+}
+
+void unbind_CudaBVHTexture(void) { compat_check(mrt_unbind_bvh(), __FILE__, __LINE__); }
+
+float launch_tracingKernel(int32_t nthreads, int32_t* blockSize, int numRays, bool anyHit, void* rays,
+                           void* results, void* nodesA, void* nodesB, void* nodesC, void* nodesD, void* trisA,
+                           void* trisB, void* trisC, int32_t* triIndices) {
+    // The reference ignored nthreads/blockSize (CudaKernel::setGrid rewrote
+    // them) and read the BVH through the textures bound earlier; the node/tri
+    // pointers are accepted for ABI compatibility only.
+    (void)nthreads; (void)blockSize; (void)nodesA; (void)nodesB; (void)nodesC; (void)nodesD;
+    (void)trisA; (void)trisB; (void)trisC; (void)triIndices;
+    float ms = 0.0f;
+    compat_check(mrt_trace(rays, results, numRays, anyHit ? 1 : 0, nullptr, &ms), __FILE__, __LINE__);
+    return ms;
+}
+
+void copy_tracing_results(void* result_host, void* result_dev, int32_t size) {
+    const hipError_t e = hipMemcpy(result_host, result_dev, (size_t)size * 16u, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) compat_check(hipFail(e, "hipMemcpy"), __FILE__, __LINE__);
+}
+
+}  // extern "C"

@@ -1,0 +1,58 @@
+// trace_kernel.hpp — launch interface between the C-ABI glue (mrt_api.cpp)
+// and the gfx950 traversal kernels (trace_kernel.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace mrt {
+
+// Bottom-of-stack marker; the traversal ends when it is popped
+// (reference CudaTracerKernels.hh:107-111 EntrypointSentinel).
+constexpr int kEntrypointSentinel = 0x76543210;
+
+// Total per-lane stack capacity (reference STACK_SIZE 64,
+// kepler_dynamic_fetch.cu:47). The top kLdsStack entries live in LDS, the
+// rest spill to a per-lane slab in HBM.
+constexpr int kStackCapacity = 64;
+constexpr int kMaxQueues = 8;
+constexpr int kQueueStrideWords = 64;      // one 256-B line per queue head
+constexpr int kBlockThreads = 256;         // 4 wave64s per workgroup
+
+// Everything one launch needs; passed by value as the kernel argument.
+struct TraceArgs {
+    const float4* rays;        // Ray[n] as 2 x float4
+    int2* results;             // RayResult[n] viewed as int2 pairs; slot 2*i = {id, t}
+    const float4* nodes;       // Compact2 nodes
+    const float4* woop;        // Woop triangles
+    const int* triIndex;       // remap table
+    uint32_t nodeBytes;        // buffer-resource ranges (range-checked loads)
+    uint32_t woopBytes;
+    int numRays;
+    int numQueues;             // 1..8 ray queues (per-XCD heads)
+    int fetchThreshold;        // refill when fewer live lanes than this
+    int totalLanes;            // grid lanes (stride of the spill slab)
+    unsigned* queues;          // numQueues heads, kQueueStrideWords apart, zeroed per launch
+    int* spill;                // (kStackCapacity - S) * totalLanes ints
+    int* status;               // [0] = stack overflow count
+    int4* stats;               // per-ray {nodes, tris, leaves, 0} (STATS variants)
+};
+
+// Variant selector (all combinations are instantiated in trace_kernel.hip).
+struct TraceVariant {
+    bool anyHit;
+    bool speculative;   // reference warp-wide postponement (ballot) vs per-lane
+    bool exactRcp;      // IEEE 1/x vs v_rcp_f32
+    bool stats;
+    int ldsStack;       // 8, 16 or 32 LDS entries per lane
+};
+
+// Launch one persistent trace. grid = number of 256-thread workgroups.
+hipError_t launch_trace(const TraceVariant& v, const TraceArgs& a, int gridBlocks, hipStream_t s);
+
+// Resident 256-thread workgroups per CU for a variant (occupancy query).
+hipError_t trace_occupancy(const TraceVariant& v, int* blocksPerCU);
+
+// Static facts about a variant's code object (for occupancy sizing/reporting).
+hipError_t trace_kernel_attributes(const TraceVariant& v, hipFuncAttributes* attr);
+
+}  // namespace mrt

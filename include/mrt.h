@@ -1,0 +1,137 @@
+/*
+ * mrt.h — C-ABI of the MI355X BVH ray-traversal engine (the hot path).
+ *
+ * This is the drop-in boundary for the reference's tracing kernel module:
+ *   reference  src/rt/kernels/CudaTracerKernels.hh:42-52   (extern "C" prototypes)
+ *   reference  src/rt/kernels/kepler_dynamic_fetch.cu:417-479 (their implementations)
+ *   caller     src/rt/cuda/CudaTracer.cc:119-177            (CudaTracer::traceBatch)
+ *
+ * Data formats are the reference's, byte for byte:
+ *   - nodes    : CudaBVH BVHLayout_Compact2 node array, 64 B per inner node
+ *                (reference src/rt/cuda/CudaBVH.hh:40-55, CudaBVH.cc:270-357)
+ *   - woop     : Woop triangle rows (Z,U,V as float4) + one float4 terminator
+ *                (x bits == 0x80000000) after every leaf
+ *   - triIndex : one int32 per woop float4 slot (origIdx for the Z row)
+ *   - rays     : Ray[n], 32 B = float4(orig.xyz, tmin) + float4(dir.xyz, tmax)
+ *                (reference src/rt/Util.hh:64-73)
+ *   - results  : RayResult[n], 16 B = int id, float t, int pad[2]; the trace
+ *                writes only {id, t} (reference src/rt/Util.hh:79-89,
+ *                CudaTracerKernels.hh:197 STORE_RESULT)
+ *
+ * All buffer pointers are DEVICE pointers owned by the caller (the library
+ * borrows them; reference ownership model CudaBVH.cc:101-109, RayBuffer.cc:42-81).
+ * Every function returns 0 on success or a positive MRT_ERR_* code; the
+ * reference instead printed and exit(-1)'d (cutil_inline_runtime.h:32-42) —
+ * the compat entry points at the bottom keep that behaviour.
+ */
+#ifndef MRT_H
+#define MRT_H
+
+#include <stdint.h>
+#include <stddef.h>
+#ifndef __cplusplus
+#include <stdbool.h>
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error codes ------------------------------------------------------ */
+enum {
+    MRT_OK = 0,
+    MRT_ERR_INVALID_ARG = 1,   /* null pointer / negative size / bad flag   */
+    MRT_ERR_NOT_BOUND = 2,     /* trace before bind (CudaTracer.cc:129)      */
+    MRT_ERR_HIP = 3,           /* a HIP runtime call failed                  */
+    MRT_ERR_NO_DEVICE = 4,     /* no GPU visible                             */
+    MRT_ERR_TOO_LARGE = 5      /* buffer beyond the 4 GiB buffer-offset range */
+};
+
+/* ---- trace flags (bit set) -------------------------------------------- */
+enum {
+    MRT_TRACE_ANY_HIT = 1u << 0,  /* any-hit early out; reference anyHit=!needClosestHit (CudaTracer.cc:172) */
+    MRT_TRACE_EXACT_RCP = 1u << 1,/* correctly rounded 1/x in the Woop test & ray setup (parity mode);
+                                     default is the hardware v_rcp_f32 (the reference used rcp.approx)  */
+    MRT_TRACE_LOCKSTEP_OFF = 1u << 2, /* per-lane (non-speculative) while-while: every lane follows the
+                                     single-ray order exactly (deterministic any-hit, exact counters)  */
+    MRT_TRACE_STATS = 1u << 3     /* also write per-ray {inner nodes, tris tested, leaves, 0} int4s     */
+};
+
+typedef struct mrt_tracer mrt_tracer;   /* one per HIP device; re-entrant per handle */
+
+/* Tuning knobs of the persistent launch (0 = library default). */
+typedef struct mrt_launch_cfg {
+    int32_t waves_per_cu;      /* persistent waves per CU (grid = CUs * waves_per_cu waves)      */
+    int32_t fetch_threshold;   /* refill a wave when fewer than this many of its 64 lanes are live
+                                  (reference DYNAMIC_FETCH_THRESHOLD 20 of 32, kepler_dynamic_fetch.cu:48) */
+    int32_t num_queues;        /* ray work queues (1..8); default 8 = one per XCD                 */
+    int32_t lds_stack;         /* traversal-stack entries per lane kept in LDS: 8, 16 or 32       */
+} mrt_launch_cfg;
+
+/* Per-launch statistics reported back to the host (optional). */
+typedef struct mrt_trace_info {
+    float   kernel_ms;         /* event-timed duration of the trace launch (if requested)        */
+    int32_t grid_waves;        /* persistent waves launched                                       */
+    int32_t block_threads;     /* threads per workgroup                                           */
+    int32_t lds_stack_entries; /* per-lane traversal-stack entries held in LDS                    */
+    int32_t stack_overflows;   /* lanes that needed more than 64 stack entries (0 for SBVH depth<=64) */
+} mrt_trace_info;
+
+/* ---- handle API -------------------------------------------------------- */
+int  mrt_tracer_create(int device, mrt_tracer** out);
+int  mrt_tracer_destroy(mrt_tracer* t);
+
+/* Bind a Compact2 BVH (device pointers, borrowed). Replaces bind_CudaBVHTexture
+ * (CudaTracerKernels.hh:44); unlike the reference it may be called again to
+ * re-bind a new BVH (the reference never re-bound, CudaTracer.cc:142-146). */
+int  mrt_tracer_bind(mrt_tracer* t,
+                     const void* nodes, int64_t nodeBytes,
+                     const void* woop, int64_t woopBytes,
+                     const int32_t* triIndex, int64_t triIndexBytes);
+int  mrt_tracer_unbind(mrt_tracer* t);
+
+int  mrt_tracer_set_config(mrt_tracer* t, const mrt_launch_cfg* cfg);
+int  mrt_tracer_get_config(const mrt_tracer* t, mrt_launch_cfg* cfg);
+
+/* Stream-ordered trace of numRays rays (device pointers). stream is a
+ * hipStream_t (NULL = the null stream). stats may be NULL unless
+ * MRT_TRACE_STATS is set (then: int32[4*numRays]). Asynchronous. */
+int  mrt_tracer_trace(mrt_tracer* t, const void* rays, void* results, int32_t numRays,
+                      uint32_t flags, int32_t* stats, void* stream);
+
+/* Same, but blocking and event-timed around the launch only — the
+ * reference's launch_tracingKernel contract (kepler_dynamic_fetch.cu:432-474). */
+int  mrt_tracer_trace_timed(mrt_tracer* t, const void* rays, void* results, int32_t numRays,
+                            uint32_t flags, int32_t* stats, void* stream, mrt_trace_info* info);
+
+/* ---- per-device convenience API (one implicit tracer per device) -------- */
+int  mrt_bind_bvh(const void* nodes, int64_t nodeBytes, const void* woop, int64_t woopBytes,
+                  const int32_t* triIndex, int64_t triIndexBytes);
+int  mrt_unbind_bvh(void);
+int  mrt_trace(const void* rays, void* results, int32_t numRays, int32_t anyHit, void* stream,
+               float* outMs /* may be NULL: then asynchronous */);
+
+/* Host-side introspection. */
+const char* mrt_error_string(int err);
+const char* mrt_last_error_detail(void);     /* thread-local text of the last failure */
+int  mrt_version(void);                      /* 100 * major + minor                     */
+int  mrt_device_count(void);
+
+/* ---- reference-compatible entry points (same names, same arguments) ----
+ * CudaTracerKernels.hh:44-52. Errors print "[file,line] (HIP error N: msg)"
+ * and exit(-1) like cutilSafeCall. float4/int4/RayResult are passed as void*
+ * and Vec2i& as a pointer to two int32 (ABI-identical). */
+void  bind_CudaBVHTexture(void* nodeBuf, int64_t nodeBufSize, void* triWoopBuf, int64_t triWoopSize,
+                          int32_t* triIndexBuf, int64_t triIndexSize);
+void  unbind_CudaBVHTexture(void);
+float launch_tracingKernel(int32_t nthreads, int32_t* blockSize, int numRays, bool anyHit,
+                           void* rays, void* results,
+                           void* nodesA, void* nodesB, void* nodesC, void* nodesD,
+                           void* trisA, void* trisB, void* trisC, int32_t* triIndices);
+void  copy_tracing_results(void* result_host, void* result_dev, int32_t size);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MRT_H */

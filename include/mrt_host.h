@@ -1,0 +1,96 @@
+/*
+ * mrt_host.h — C-ABI of the host side around the hot path: scenes, the SBVH
+ * builder, the Compact2 layout and its bvhcache .dat format, the camera and
+ * ray generation. These are the producers of the trace kernel's inputs
+ * (SURVEY.md §8f "next" rows), restating:
+ *   src/rt/Scene.cc:35-101, src/framework/io/MeshWavefrontIO.cc:258-467   (scene, OBJ)
+ *   src/rt/bvh/SplitBVHBuilder.cc:55-485, src/framework/base/Sort.cc:63-239 (SBVH)
+ *   src/rt/cuda/CudaBVH.cc:79-116,270-380, Renderer.cc:157-217            (Compact2, cache)
+ *   src/rt/ray/RayGen.cc:50-142, RayGenKernels.cu:79-227, PixelTable.cc    (ray generation)
+ * All buffers here are HOST memory. Functions return 0 or an MRTH_ERR_* code.
+ */
+#ifndef MRT_HOST_H
+#define MRT_HOST_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { MRTH_OK = 0, MRTH_ERR_INVALID_ARG = 1, MRTH_ERR_IO = 2, MRTH_ERR_GENERATOR = 3 };
+
+typedef struct mrth_scene mrth_scene;
+typedef struct mrth_bvh mrth_bvh;
+
+typedef struct mrth_camera {
+    float position[3];
+    float forward[3];
+    float up[3];
+    float fov_deg;      /* vertical field of view */
+    float near_dist;
+    float far_dist;
+} mrth_camera;
+
+typedef struct mrth_build_params {
+    float sah_node_cost;      /* 1.0 */
+    float sah_triangle_cost;  /* 1.0 */
+    int32_t min_leaf_size;    /* 1   (Renderer.cc:54) */
+    int32_t max_leaf_size;    /* 8   (Renderer.cc:54) */
+    float split_alpha;        /* 1e-5 (BVH.hh BuildParams) */
+    int32_t threads;          /* 0 = all cores; output is independent of it */
+} mrth_build_params;
+
+typedef struct mrth_bvh_stats {
+    int64_t inner_nodes;
+    int64_t leaf_nodes;
+    int64_t tri_refs;
+    int64_t max_depth;
+    float sah_cost;
+    double build_seconds;
+} mrth_bvh_stats;
+
+/* ---- scenes -------------------------------------------------------------- */
+/* name: "mori" | "bunny" | "conference" | "sponza" | "hairball" (published
+ * triangle counts), "sphere" (param = rings), "random" (param = triangles). */
+int  mrth_scene_synthetic(const char* name, int64_t param, uint64_t seed, mrth_scene** out);
+int  mrth_scene_load_obj(const char* path, mrth_scene** out);
+int  mrth_scene_from_arrays(const float* vertices, int64_t numVertices, const int32_t* triangles,
+                            int64_t numTriangles, mrth_scene** out);
+void mrth_scene_destroy(mrth_scene* s);
+int64_t mrth_scene_num_triangles(const mrth_scene* s);
+int64_t mrth_scene_num_vertices(const mrth_scene* s);
+int  mrth_scene_copy_arrays(const mrth_scene* s, float* vertices /* 3*nv or NULL */,
+                            int32_t* triangles /* 3*nt or NULL */, float* normals /* 3*nt or NULL */);
+int  mrth_scene_camera(const mrth_scene* s, mrth_camera* cam, float* aoRadius);
+
+/* ---- BVH (SBVH build -> Compact2 host buffers) ---------------------------- */
+void mrth_default_build_params(mrth_build_params* p);
+int  mrth_bvh_build(const mrth_scene* s, const mrth_build_params* p /* NULL = defaults */, mrth_bvh** out);
+int  mrth_bvh_load(const char* datPath, mrth_bvh** out);
+int  mrth_bvh_save(const mrth_bvh* b, const char* datPath);
+int  mrth_bvh_from_buffers(const void* nodes, int64_t nodeBytes, const void* woop, int64_t woopBytes,
+                           const int32_t* triIndex, int64_t triIndexBytes, mrth_bvh** out);
+void mrth_bvh_destroy(mrth_bvh* b);
+int  mrth_bvh_buffers(const mrth_bvh* b, const void** nodes, int64_t* nodeBytes, const void** woop,
+                      int64_t* woopBytes, const int32_t** triIndex, int64_t* triIndexBytes);
+int  mrth_bvh_get_stats(const mrth_bvh* b, mrth_bvh_stats* out);
+/* Woop rows (Z,U,V; 12 floats) of one triangle, CudaBVH::woopifyTri. */
+void mrth_woopify(const float v0[3], const float v1[3], const float v2[3], float out[12]);
+
+/* ---- rays (Ray = 8 floats, RayResult = 4 x 32 bit) ------------------------ */
+int  mrth_pixel_table(int32_t w, int32_t h, int32_t* indexToPixel /* w*h */);
+int  mrth_primary_rays(const mrth_camera* cam, int32_t w, int32_t h, void* rays /* w*h Ray */,
+                       int32_t* slotToId /* w*h or NULL */);
+int  mrth_ao_rays(const void* primaryRays, const void* primaryResults, int64_t numPrimary,
+                  const mrth_scene* s, int32_t numSamples, float maxDist, uint32_t seed,
+                  void* outRays /* numPrimary * numSamples Ray */);
+int64_t mrth_count_hits(const void* results, int64_t n);
+
+const char* mrth_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MRT_HOST_H */
