@@ -1,0 +1,62 @@
+"""The C-ABI libraries load and export every symbol their headers declare
+(CPU-only: no kernel is launched)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from mrt import _lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions(header):
+    text = open(os.path.join(REPO, "include", header)).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\(", text)
+    skip = {"if", "defined", "sizeof"}
+    return sorted({n for n in names if n not in skip and not n.isupper()})
+
+
+@pytest.mark.parametrize("header,path", [("mrt.h", _lib.TRACE_LIB_PATH), ("mrt_host.h", _lib.HOST_LIB_PATH)])
+def test_every_declared_symbol_is_exported(header, path):
+    lib = C.CDLL(path)
+    names = declared_functions(header)
+    assert len(names) > 10
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, f"{os.path.basename(path)} lacks {missing}"
+
+
+@pytest.mark.parametrize("header,table", [("mrt.h", _lib.TRACE_SYMBOLS), ("mrt_host.h", _lib.HOST_SYMBOLS)])
+def test_python_bindings_cover_the_header(header, table):
+    assert sorted(n for n, _, _ in table) == declared_functions(header)
+
+
+def test_reference_compat_names_present():
+    # CudaTracerKernels.hh:44-52
+    lib = _lib.trace_lib()
+    for n in ("bind_CudaBVHTexture", "unbind_CudaBVHTexture", "launch_tracingKernel", "copy_tracing_results"):
+        assert hasattr(lib, n)
+
+
+def test_error_strings_and_version():
+    lib = _lib.trace_lib()
+    assert lib.mrt_version() >= 100
+    assert lib.mrt_error_string(0) == b"ok"
+    assert lib.mrt_error_string(2) == b"no BVH bound"
+
+
+def test_invalid_arguments_rejected_without_gpu():
+    lib = _lib.trace_lib()
+    out = C.c_void_p()
+    assert lib.mrt_tracer_create(0, None) == 1           # null out pointer
+    rc = lib.mrt_tracer_create(0, C.byref(out))
+    if lib.mrt_device_count() == 0:
+        assert rc == 4                                   # MRT_ERR_NO_DEVICE
+        assert out.value is None
+    else:
+        assert rc == 0
+        lib.mrt_tracer_destroy(out)
+    assert lib.mrt_tracer_trace(None, None, None, 1, 0, None, None) == 1
+    assert lib.mrt_tracer_bind(None, None, 0, None, 0, None, 0) == 1

@@ -1,0 +1,274 @@
+"""GPU parity: the HIP traversal behind the C-ABI against the CPU oracle.
+
+Contract:
+  * exact-rcp mode (MRT_TRACE_EXACT_RCP), per-lane order (LOCKSTEP_OFF):
+        id, t and the per-ray counters bit-identical to the oracle, closest and any-hit;
+  * exact-rcp, speculative (the reference's warp-wide postponement):
+        closest hit: id and t bit-identical;  any hit: hit/miss identical and the
+        reported triangle is a valid hit whose t the oracle's Woop test reproduces bit-exactly;
+  * fast rcp (v_rcp_f32): ids identical except exact-t ties, |dt| <= 2 ulp
+        (v_rcp_f32 is within 1 ulp of 1/x; one more rounding in Oz * rcp(Dz)).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+import kat  # noqa: E402
+import mrt  # noqa: E402
+import oracle_lib as O  # noqa: E402
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def tracer():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mrt.tracer import Tracer
+    return Tracer(0)
+
+
+def gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=True, stats=False):
+    from mrt.tracer import GpuBvh, RayBuffer
+    g = GpuBvh(bufs)
+    tracer.set_bvh(g)
+    rb = RayBuffer(rays, need_closest_hit=not any_hit)
+    rb.results.fill_(0x5A5A5A5A)   # pads must survive: the trace writes {id, t} only
+    tracer.trace_batch(rb, exact_rcp=exact, speculative=spec, stats=stats)
+    r = rb.results_numpy()
+    assert (r[:, 2:] == 0x5A5A5A5A).all(), "RayResult padding was overwritten"
+    return r, (rb.stats.cpu().numpy() if stats else None)
+
+
+def ulp_diff(a_bits, b_bits):
+    a = a_bits.astype(np.int64)
+    b = b_bits.astype(np.int64)
+    a = np.where(a < 0, -(a & 0x7FFFFFFF), a)
+    b = np.where(b < 0, -(b & 0x7FFFFFFF), b)
+    return np.abs(a - b)
+
+
+def assert_valid_hits(rays, res, oracle_res, bufs):
+    """Every differing any-hit result is a genuine hit the oracle's Woop test reproduces."""
+    nodes, woop, tri = bufs
+    diff = np.nonzero((res[:, 0] != oracle_res[:, 0]) | (res[:, 1] != oracle_res[:, 1]))[0]
+    assert np.array_equal(res[:, 0] == -1, oracle_res[:, 0] == -1), "hit/miss differs"
+    woop4 = woop.reshape(-1, 4)
+    for i in diff[:2000]:
+        # find a woop slot holding triangle res[i,0] whose Woop test gives exactly res t
+        cand = np.nonzero((tri == res[i, 0]) & (woop4[:, 0] != np.int32(-2147483648)))[0]
+        ok = False
+        for s in cand:
+            hit, t = O.woop_hit(rays[i], woop, s, float(rays[i][7]))
+            if hit and np.float32(t).view(np.int32) == res[i, 1]:
+                ok = True
+                break
+        assert ok, f"ray {i}: GPU any-hit ({res[i, 0]}, {res[i, 1]}) is not a valid hit"
+
+
+# ---------------------------------------------------------------- known answers
+@pytest.mark.parametrize("exact", [True, False])
+@pytest.mark.parametrize("spec", [True, False])
+@pytest.mark.parametrize("case", kat.cases(), ids=lambda c: c[0])
+def test_known_answers(tracer, case, spec, exact):
+    name, scene, rays, any_hit, expected = case
+    res, _ = gpu_trace(tracer, scene(), np.stack(rays), any_hit, exact=exact, spec=spec)
+    for (rid, rt), got in zip(expected, res):
+        assert got[0] == rid, name
+        assert got[1] == kat.f2i(rt), name
+
+
+# ---------------------------------------------------------------- golden fixtures
+@pytest.mark.parametrize("fname", sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz")))
+def test_golden_fixtures(tracer, fname):
+    g = np.load(os.path.join(GOLDEN, fname))
+    bufs = (g["nodes"], g["woop"], g["tri_index"])
+    any_hit = bool(g["any_hit"])
+    res, st = gpu_trace(tracer, bufs, g["rays"], any_hit, exact=True, spec=False, stats=True)
+    assert np.array_equal(res[:, :2], g["results"][:, :2])
+    assert np.array_equal(st[:, :3], g["stats"][:, :3])
+    res2, _ = gpu_trace(tracer, bufs, g["rays"], any_hit, exact=True, spec=True)
+    if any_hit:
+        assert_valid_hits(g["rays"], res2, g["results"], bufs)
+    else:
+        assert np.array_equal(res2[:, :2], g["results"][:, :2])
+
+
+# ---------------------------------------------------------------- synthetic scenes
+SCENE_CACHE = {}
+
+
+def scene_setup(name, w, h, kind):
+    key = (name, w, h, kind)
+    if key not in SCENE_CACHE:
+        scene = mrt.Scene.synthetic(name, 0, 1)
+        bufs = mrt.Bvh.build(scene).buffers()
+        cam, ao = scene.camera()
+        rays, _ = mrt.primary_rays(cam, w, h)
+        if kind != "primary":
+            prim, _, _ = O.trace(rays, *bufs, threads=8)
+            rays = mrt.ao_rays(rays, prim, scene, ao if kind == "ao" else cam.far)
+        any_hit = kind == "ao"
+        want, st, _ = O.trace(rays, *bufs, any_hit=any_hit, stats=True, threads=8)
+        SCENE_CACHE[key] = (bufs, rays, any_hit, want, st)
+    return SCENE_CACHE[key]
+
+
+WORKLOADS = [("bunny", 320, 240, "primary"), ("conference", 256, 192, "ao"), ("sponza", 256, 192, "diffuse"),
+             ("conference", 256, 192, "diffuse"), ("mori", 256, 192, "ao")]
+
+
+@pytest.mark.parametrize("wl", WORKLOADS, ids=lambda w: "-".join(map(str, w)))
+def test_exact_lockstep_off_is_bit_identical_with_counters(tracer, wl):
+    bufs, rays, any_hit, want, st = scene_setup(*wl)
+    res, gst = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=False, stats=True)
+    assert np.array_equal(res[:, :2], want[:, :2])
+    assert np.array_equal(gst[:, :3], st[:, :3])
+
+
+@pytest.mark.parametrize("wl", WORKLOADS, ids=lambda w: "-".join(map(str, w)))
+def test_exact_speculative(tracer, wl):
+    bufs, rays, any_hit, want, _ = scene_setup(*wl)
+    res, _ = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=True)
+    if any_hit:
+        assert_valid_hits(rays, res, want, bufs)
+    else:
+        assert np.array_equal(res[:, :2], want[:, :2])
+
+
+@pytest.mark.parametrize("wl", WORKLOADS, ids=lambda w: "-".join(map(str, w)))
+def test_fast_rcp_within_tolerance(tracer, wl):
+    bufs, rays, any_hit, want, _ = scene_setup(*wl)
+    res, _ = gpu_trace(tracer, bufs, rays, any_hit, exact=False, spec=True)
+    assert np.array_equal(res[:, 0] == -1, want[:, 0] == -1)
+    hit = want[:, 0] != -1
+    if not any_hit:
+        id_eq = (res[:, 0] == want[:, 0]).mean()
+        assert id_eq >= 1.0 - 1e-4, f"id agreement {id_eq}"
+        same = hit & (res[:, 0] == want[:, 0])
+        assert ulp_diff(res[same, 1], want[same, 1]).max(initial=0) <= 2
+    assert np.array_equal(res[~hit, 1], want[~hit, 1])   # misses keep tmax exactly
+
+
+# ---------------------------------------------------------------- launch configs
+@pytest.mark.parametrize("cfg", [dict(lds_stack=8), dict(lds_stack=32), dict(waves_per_cu=8),
+                                 dict(num_queues=1), dict(fetch_threshold=0), dict(fetch_threshold=64),
+                                 dict(waves_per_cu=4, lds_stack=8, num_queues=3)],
+                         ids=lambda c: ",".join(f"{k}={v}" for k, v in c.items()))
+def test_launch_configs_do_not_change_results(tracer, cfg):
+    bufs, rays, any_hit, want, st = scene_setup("conference", 256, 192, "diffuse")
+    saved = tracer.config()
+    try:
+        tracer.set_config(**cfg)
+        res, gst = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=False, stats=True)
+        assert np.array_equal(res[:, :2], want[:, :2]) and np.array_equal(gst[:, :3], st[:, :3])
+        res2, _ = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=True)
+        assert np.array_equal(res2[:, :2], want[:, :2])
+    finally:
+        tracer.set_config(**saved)
+
+
+def test_invalid_config_rejected(tracer):
+    from mrt._lib import MrtError
+    with pytest.raises(MrtError):
+        tracer.set_config(lds_stack=12)
+    with pytest.raises(MrtError):
+        tracer.set_config(num_queues=9)
+
+
+# ---------------------------------------------------------------- edge cases
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1000, 4097])
+def test_ragged_batch_sizes(tracer, n):
+    bufs, rays, any_hit, want, _ = scene_setup("bunny", 320, 240, "primary")
+    res, _ = gpu_trace(tracer, bufs, rays[:n], False, exact=True, spec=True)
+    assert np.array_equal(res[:, :2], want[:n, :2])
+
+
+def test_empty_batch_returns_zero_ms(tracer):
+    from mrt.tracer import GpuBvh, RayBuffer
+    tracer.set_bvh(GpuBvh(kat.scene_two_floors()))
+    rb = RayBuffer(np.zeros((0, 8), np.float32))
+    assert tracer.trace_batch(rb) == 0.0
+
+
+def test_trace_before_bind_fails(tracer):
+    from mrt._lib import MrtError
+    from mrt.tracer import RayBuffer, Tracer
+    t = Tracer(0)
+    rb = RayBuffer(np.zeros((4, 8), np.float32))
+    with pytest.raises(MrtError):
+        t.trace_batch(rb)
+    lib = t.lib
+    rc = lib.mrt_tracer_trace(t._h, rb.rays.data_ptr(), rb.results.data_ptr(), 4, 0, None, None)
+    assert rc == 2   # MRT_ERR_NOT_BOUND
+
+
+def test_rebinding_a_different_bvh(tracer):
+    b1, rays1, _, want1, _ = scene_setup("bunny", 320, 240, "primary")
+    b2, rays2, any2, want2, _ = scene_setup("mori", 256, 192, "ao")
+    r1, _ = gpu_trace(tracer, b1, rays1, False)
+    r2, _ = gpu_trace(tracer, b2, rays2, True, spec=False)
+    r1b, _ = gpu_trace(tracer, b1, rays1, False)
+    assert np.array_equal(r1[:, :2], want1[:, :2]) and np.array_equal(r1b[:, :2], want1[:, :2])
+    assert np.array_equal(r2[:, :2], want2[:, :2])
+
+
+def test_reference_compat_entry_points(tracer):
+    """bind_CudaBVHTexture + launch_tracingKernel + copy_tracing_results, exactly
+    the reference call sequence of CudaTracer::traceBatch (CudaTracer.cc:142-177)."""
+    from mrt import _lib
+    bufs, rays, any_hit, want, _ = scene_setup("bunny", 320, 240, "primary")
+    lib = _lib.trace_lib()
+    nodes, woop, tri = (torch.from_numpy(b).cuda() for b in bufs)
+    r = torch.from_numpy(rays).cuda()
+    out = torch.zeros((len(rays), 4), dtype=torch.int32, device="cuda")
+    lib.bind_CudaBVHTexture(nodes.data_ptr(), nodes.numel() * 4, woop.data_ptr(), woop.numel() * 4, tri.data_ptr(),
+                            tri.numel() * 4)
+    block = (C.c_int32 * 2)(32, 4)
+    ms = lib.launch_tracingKernel(180 * 128, block, len(rays), False, r.data_ptr(), out.data_ptr(),
+                                  nodes.data_ptr(), None, None, None, woop.data_ptr(), None, None, tri.data_ptr())
+    assert ms > 0.0
+    host = np.zeros((len(rays), 4), np.int32)
+    lib.copy_tracing_results(host.ctypes.data, out.data_ptr(), len(rays))
+    # The compat launch keeps the reference's fast reciprocal (rcp.approx there,
+    # v_rcp_f32 here): ids identical, t within the fast-mode tolerance.
+    assert np.array_equal(host[:, 0], want[:, 0])
+    assert ulp_diff(host[:, 1], want[:, 1]).max() <= 2
+    lib.unbind_CudaBVHTexture()
+
+
+def test_async_trace_on_a_side_stream(tracer):
+    from mrt.tracer import GpuBvh, RayBuffer
+    bufs, rays, any_hit, want, _ = scene_setup("sponza", 256, 192, "diffuse")
+    tracer.set_bvh(GpuBvh(bufs))
+    s = torch.cuda.Stream()
+    rb = RayBuffer(rays, need_closest_hit=True)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s):
+        tracer.trace_async(rb, exact_rcp=True, stream=s)
+    s.synchronize()
+    assert np.array_equal(rb.results_numpy()[:, :2], want[:, :2])
+
+
+# ---------------------------------------------------------------- full size
+def test_full_size_bunny_primary_1024x768(tracer):
+    """The bench's headline workload, bit-identical to the oracle on every ray."""
+    bufs, rays, any_hit, want, st = scene_setup("bunny", 1024, 768, "primary")
+    res, _ = gpu_trace(tracer, bufs, rays, False, exact=True, spec=True)
+    assert np.array_equal(res[:, :2], want[:, :2])
+    res2, gst = gpu_trace(tracer, bufs, rays, False, exact=True, spec=False, stats=True)
+    assert np.array_equal(gst[:, :3], st[:, :3])
+
+
+def test_repeated_launches_are_deterministic(tracer):
+    bufs, rays, any_hit, want, _ = scene_setup("conference", 256, 192, "ao")
+    a, _ = gpu_trace(tracer, bufs, rays, True, exact=True, spec=False)
+    for _ in range(3):
+        b, _ = gpu_trace(tracer, bufs, rays, True, exact=True, spec=False)
+        assert np.array_equal(a[:, :2], b[:, :2])

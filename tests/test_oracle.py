@@ -1,0 +1,98 @@
+"""CPU oracle (oracle/trace_oracle.c) pinned against hand-derived known
+answers and the committed golden fixtures; plus BVH-independence against a
+brute-force scan of every triangle."""
+import os
+
+import numpy as np
+import pytest
+
+import kat
+import mrt
+import oracle_lib as O
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.mark.parametrize("case", kat.cases(), ids=lambda c: c[0])
+def test_known_answers(case):
+    name, scene, rays, any_hit, expected = case
+    nodes, woop, tri = scene()
+    res, stats, _ = O.trace(np.stack(rays), nodes, woop, tri, any_hit=any_hit, stats=True)
+    for (rid, rt), got in zip(expected, res):
+        assert got[0] == rid, name
+        assert got[1] == kat.f2i(rt), f"{name}: t={got[1:2].view(np.float32)[0]} want {rt}"
+    assert (stats[:, 3] == 0).all()
+
+
+def test_kat_woop_rows_match_the_product_woopify():
+    """mrth_woopify (CudaBVH::woopifyTri restated, with the reference's
+    cofactor-inverse quirk) equals the exact inverse on exactly representable triangles."""
+    for v0, v1, v2 in [((0, 0, 0), (1, 0, 0), (0, 1, 0)), ((2, 0, -1), (4, 0, -1), (2, 2, -1)),
+                       ((0, 0, -3), (1, 0, -3), (0, 1, -3))]:
+        assert np.array_equal(mrt.woopify(v0, v1, v2), kat.woop_rows(v0, v1, v2))
+
+
+def _golden_files():
+    return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz"))
+
+
+@pytest.mark.parametrize("fname", _golden_files())
+def test_oracle_reproduces_golden_fixture(fname):
+    g = np.load(os.path.join(GOLDEN, fname))
+    res, stats, _ = O.trace(g["rays"], g["nodes"], g["woop"], g["tri_index"], any_hit=bool(g["any_hit"]),
+                            stats=True, threads=4)
+    assert np.array_equal(res[:, :2], g["results"][:, :2])
+    assert np.array_equal(stats[:, :3], g["stats"][:, :3])
+
+
+@pytest.mark.parametrize("fname", _golden_files())
+def test_builder_reproduces_golden_compact2(fname):
+    """The SBVH + Compact2 bytes of the fixture scene are reproducible (determinism pin)."""
+    g = np.load(os.path.join(GOLDEN, fname))
+    scene = mrt.Scene.synthetic(str(g["scene"]), int(g["param"]), int(g["seed"]))
+    nodes, woop, tri = mrt.Bvh.build(scene).buffers()
+    assert np.array_equal(nodes, g["nodes"]) and np.array_equal(woop, g["woop"]) and np.array_equal(tri, g["tri_index"])
+
+
+@pytest.mark.parametrize("scene_name,param", [("sphere", 20), ("random", 2000), ("mori", 0)])
+def test_closest_hit_equals_brute_force(scene_name, param):
+    scene = mrt.Scene.synthetic(scene_name, param, 3)
+    nodes, woop, tri = mrt.Bvh.build(scene).buffers()
+    cam, _ = scene.camera()
+    rays, _ = mrt.primary_rays(cam, 80, 60)
+    res, _, _ = O.trace(rays, nodes, woop, tri, threads=4)
+    bf = O.brute_force(rays, woop, tri)
+    same = (res[:, 0] == bf[:, 0]) & (res[:, 1] == bf[:, 1])
+    # Any difference must be an exact-t tie between two valid triangles.
+    for i in np.nonzero(~same)[0]:
+        assert res[i, 1] == bf[i, 1], f"ray {i}: BVH t differs from brute force"
+    assert same.mean() > 0.999
+
+
+def test_any_hit_agrees_with_closest_on_hit_or_miss():
+    scene = mrt.Scene.synthetic("random", 3000, 5)
+    nodes, woop, tri = mrt.Bvh.build(scene).buffers()
+    cam, _ = scene.camera()
+    rays, _ = mrt.primary_rays(cam, 64, 48)
+    closest, _, _ = O.trace(rays, nodes, woop, tri)
+    anyh, _, _ = O.trace(rays, nodes, woop, tri, any_hit=True)
+    assert np.array_equal(closest[:, 0] == -1, anyh[:, 0] == -1)
+    # an any-hit t is a real hit, never closer than the closest one
+    hit = closest[:, 0] != -1
+    assert (anyh[hit, 1].view(np.float32) >= closest[hit, 1].view(np.float32)).all()
+
+
+def test_threads_do_not_change_results():
+    scene = mrt.Scene.synthetic("mori", 0, 1)
+    nodes, woop, tri = mrt.Bvh.build(scene).buffers()
+    cam, _ = scene.camera()
+    rays, _ = mrt.primary_rays(cam, 128, 96)
+    a, sa, _ = O.trace(rays, nodes, woop, tri, stats=True, threads=1)
+    b, sb, _ = O.trace(rays, nodes, woop, tri, stats=True, threads=8)
+    assert np.array_equal(a, b) and np.array_equal(sa, sb)
+
+
+def test_empty_batch():
+    nodes, woop, tri = kat.scene_two_floors()
+    res, _, _ = O.trace(np.zeros((0, 8), np.float32), nodes, woop, tri)
+    assert res.shape == (0, 4)

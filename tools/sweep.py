@@ -1,0 +1,59 @@
+"""Launch-config sweep of the trace kernel (GPU tuning aid, not part of the product).
+
+python tools/sweep.py [--workloads a,b] [--configs JSON-list]
+Prints one line per (workload, config): median event-timed ms per launch over
+--reps launches and Mrays/s (rays counted as in bench.py)."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "gpu-ray-tracing_amd"))
+
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workloads", default="bunny-primary-1024x768,bunny-primary-640x480,conference-ao-640x480,"
+                                           "sponza-diffuse-640x480")
+    ap.add_argument("--configs", default='[{}, {"waves_per_cu": 8}, {"waves_per_cu": 16}, {"fetch_threshold": 0},'
+                                         ' {"fetch_threshold": 56}, {"num_queues": 1}, {"lds_stack": 32},'
+                                         ' {"lds_stack": 8}]')
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--rcp", default="exact")
+    ap.add_argument("--spec", type=int, default=1)
+    args = ap.parse_args()
+    import torch
+    from mrt.tracer import Tracer
+    torch.cuda.set_device(0)
+    tracer = Tracer(0)
+    base = tracer.config()
+    for wl in args.workloads.split(","):
+        scene, bufs, _, _ = bench.bvh_for(bench.WORKLOADS[wl][0], 1, 0)
+        batches = bench.Batches(wl, scene, bufs, tracer)
+        for cfg in json.loads(args.configs):
+            tracer.set_config(**{**base, **cfg})
+            s = torch.cuda.current_stream()
+            ms = []
+            for i in range(args.reps + 3):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(s)
+                for rb, _ in batches.batches:
+                    tracer.trace_async(rb, exact_rcp=(args.rcp == "exact"), speculative=bool(args.spec), stream=s)
+                b.record(s)
+                b.synchronize()
+                if i >= 3:
+                    ms.append(a.elapsed_time(b))
+            med = float(np.median(ms))
+            print(f"{wl:28s} {json.dumps(cfg):40s} {med:8.4f} ms  {batches.rays_counted / med / 1e3:9.1f} Mrays/s "
+                  f"(min {min(ms):.4f})", flush=True)
+        tracer.set_config(**base)
+
+
+if __name__ == "__main__":
+    main()
