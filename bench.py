@@ -64,6 +64,16 @@ WORKLOADS = {
     "hairball-diffuse-1920x1080": ("hairball", 1920, 1080, "diffuse", 1),
 }
 HEADLINE = "bunny-primary-1024x768"
+
+
+def workload_spec(name):
+    """WORKLOADS entry, or a parsed '<scene>-<primary|ao|diffuse|diffuseN>-<W>x<H>' name."""
+    if name in WORKLOADS:
+        return WORKLOADS[name]
+    scene, kind, res = name.split("-")
+    w, h = (int(v) for v in res.split("x"))
+    bounces = int(kind[7:]) if kind.startswith("diffuse") and len(kind) > 7 else 1
+    return (scene, w, h, kind.rstrip("0123456789"), bounces)
 EXTRA_N1 = ["bunny-primary-640x480", "conference-ao-640x480", "sponza-diffuse-640x480", "sponza-diffuse2-640x480"]
 
 
@@ -120,7 +130,7 @@ class Batches:
     def __init__(self, name, scene, bufs, tracer):
         import mrt
         from mrt.tracer import GpuBvh, RayBuffer
-        sname, w, h, kind, bounces = WORKLOADS[name]
+        sname, w, h, kind, bounces = workload_spec(name)
         self.name, self.kind, self.w, self.h = name, kind, w, h
         self.gbvh = GpuBvh(bufs)
         tracer.set_bvh(self.gbvh)
@@ -224,7 +234,7 @@ def cpu_baseline(batches, bufs, threads):
 
 
 def run_workload(name, tracer, world, rank, steps, warmup, exact, want_cpu):
-    scene_name = WORKLOADS[name][0]
+    scene_name = workload_spec(name)[0]
     scene, bufs, bstats, build_s = bvh_for(scene_name, world, rank)
     batches = Batches(name, scene, bufs, tracer)
     alg_bytes, n_nodes, n_tris, n_leaves = algorithmic_bytes(tracer, batches)
@@ -264,7 +274,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default=HEADLINE, choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default=HEADLINE, help="a WORKLOADS key or <scene>-<ray>-<W>x<H>")
     ap.add_argument("--rcp", default="exact", choices=["exact", "fast"],
                     help="exact = correctly rounded 1/x (bit-identical to the oracle); fast = v_rcp_f32")
     ap.add_argument("--extra", dest="extra", action="store_true", default=None,
@@ -321,9 +331,9 @@ def main():
             "vs_baseline": round(head["value"] / ref, 3) if ref else None,
             "dtype": "f32",
             "data": "synthetic (deterministic stand-in scene with the README triangle count; host-generated rays)",
-            "config": {"workload": args.workload, "scene": WORKLOADS[args.workload][0],
-                       "scene_tris": head["scene_tris"], "width": WORKLOADS[args.workload][1],
-                       "height": WORKLOADS[args.workload][2], "ray_type": WORKLOADS[args.workload][3],
+            "config": {"workload": args.workload, "scene": workload_spec(args.workload)[0],
+                       "scene_tris": head["scene_tris"], "width": workload_spec(args.workload)[1],
+                       "height": workload_spec(args.workload)[2], "ray_type": workload_spec(args.workload)[3],
                        "rays_per_gpu": head["rays_counted"], "rcp": args.rcp,
                        "parallelism": f"rays replicated-BVH x{world} (weak, no collective in step)",
                        "tracer": tracer.config()},

@@ -75,7 +75,7 @@ struct DeviceGuard {
 
 mrt_launch_cfg default_cfg() {
     mrt_launch_cfg c;
-    c.waves_per_cu = 32;
+    c.waves_per_cu = 0;   // auto: sized from the batch (grid_blocks)
     c.fetch_threshold = 40;
     c.num_queues = 8;
     c.lds_stack = 16;
@@ -83,7 +83,7 @@ mrt_launch_cfg default_cfg() {
 }
 
 bool valid_cfg(const mrt_launch_cfg& c) {
-    return c.waves_per_cu >= 4 && c.waves_per_cu <= 32 && c.fetch_threshold >= 0 && c.fetch_threshold <= 64 &&
+    return (c.waves_per_cu == 0 || (c.waves_per_cu >= 4 && c.waves_per_cu <= 32)) && c.fetch_threshold >= 0 && c.fetch_threshold <= 64 &&
            c.num_queues >= 1 && c.num_queues <= mrt::kMaxQueues &&
            (c.lds_stack == 8 || c.lds_stack == 16 || c.lds_stack == 32);
 }
@@ -98,12 +98,27 @@ mrt::TraceVariant variant_for(const mrt_tracer* t, uint32_t flags) {
     return v;
 }
 
+// Rays per lane the automatic grid aims for: a frame-sized batch is bound by
+// its slowest rays, whose step latency grows with the number of co-resident
+// waves, so small batches get fewer waves per CU; big batches fill the CU.
+// Measured on MI355X (tools/sweep.py, profiles/round1_sweep.txt): 8 waves/CU
+// is best up to ~1M rays (bunny primary 1024x768, conference AO), 16 at 3M,
+// 32 at 12M rays.
+constexpr int kAutoRaysPerLane = 12;
+constexpr int kAutoMinWaves = 8;
+
 // Persistent grid: as many 256-thread workgroups per CU as the config asks for
-// and the code object's occupancy admits; every workgroup is resident at once.
-int grid_blocks(const mrt_tracer* t, const mrt::TraceVariant& v, int* outBlocksPerCU) {
+// (or the batch size suggests) and the code object's occupancy admits; every
+// workgroup is resident at once.
+int grid_blocks(const mrt_tracer* t, const mrt::TraceVariant& v, int numRays, int* outBlocksPerCU) {
     int occ = 0;
     if (mrt::trace_occupancy(v, &occ) != hipSuccess || occ <= 0) occ = 1;
-    const int want = std::max(1, t->cfg.waves_per_cu / (mrt::kBlockThreads / 64));
+    int waves = t->cfg.waves_per_cu;
+    if (waves == 0) {
+        const long long lanesPerCU = (long long)numRays / kAutoRaysPerLane / std::max(1, t->numCUs);
+        waves = (int)std::min<long long>(32, std::max<long long>(kAutoMinWaves, (lanesPerCU + 63) / 64));
+    }
+    const int want = std::max(1, (waves + 3) / (mrt::kBlockThreads / 64));
     const int perCU = std::min(want, occ);
     if (outBlocksPerCU) *outBlocksPerCU = perCU;
     return perCU * t->numCUs;
@@ -145,7 +160,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     DeviceGuard guard(t->device);
     const mrt::TraceVariant v = variant_for(t, flags);
     int perCU = 0;
-    const int blocks = grid_blocks(t, v, &perCU);
+    const int blocks = grid_blocks(t, v, numRays, &perCU);
     const int totalLanes = blocks * mrt::kBlockThreads;
     if (int rc = ensure_workspace(t, totalLanes, v.ldsStack)) return rc;
 

@@ -13,7 +13,7 @@ import ctypes as C
 import os
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_DIR = os.path.join(PKG_DIR, "lib")
+LIB_DIR = os.environ.get("MRT_LIB_DIR") or os.path.join(PKG_DIR, "lib")
 TRACE_LIB_PATH = os.path.join(LIB_DIR, "libmrt.so")
 HOST_LIB_PATH = os.path.join(LIB_DIR, "libmrt_host.so")
 

@@ -54,14 +54,14 @@ enum {
                                      default is the hardware v_rcp_f32 (the reference used rcp.approx)  */
     MRT_TRACE_LOCKSTEP_OFF = 1u << 2, /* per-lane (non-speculative) while-while: every lane follows the
                                      single-ray order exactly (deterministic any-hit, exact counters)  */
-    MRT_TRACE_STATS = 1u << 3     /* also write per-ray {inner nodes, tris tested, leaves, 0} int4s     */
+    MRT_TRACE_STATS = 1u << 3     /* also write per-ray {inner nodes, tris tested, leaves, latency in 10 ns ticks} int4s */
 };
 
 typedef struct mrt_tracer mrt_tracer;   /* one per HIP device; re-entrant per handle */
 
 /* Tuning knobs of the persistent launch (0 = library default). */
 typedef struct mrt_launch_cfg {
-    int32_t waves_per_cu;      /* persistent waves per CU (grid = CUs * waves_per_cu waves)      */
+    int32_t waves_per_cu;      /* persistent waves per CU (grid = CUs * waves_per_cu); 0 = auto (by batch size) */
     int32_t fetch_threshold;   /* refill a wave when fewer than this many of its 64 lanes are live
                                   (reference DYNAMIC_FETCH_THRESHOLD 20 of 32, kepler_dynamic_fetch.cu:48) */
     int32_t num_queues;        /* ray work queues (1..8); default 8 = one per XCD                 */

@@ -34,7 +34,7 @@ def main():
     tracer = Tracer(0)
     base = tracer.config()
     for wl in args.workloads.split(","):
-        scene, bufs, _, _ = bench.bvh_for(bench.WORKLOADS[wl][0], 1, 0)
+        scene, bufs, _, _ = bench.bvh_for(bench.workload_spec(wl)[0], 1, 0)
         batches = bench.Batches(wl, scene, bufs, tracer)
         for cfg in json.loads(args.configs):
             tracer.set_config(**{**base, **cfg})
