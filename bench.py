@@ -77,6 +77,22 @@ def workload_spec(name):
 EXTRA_N1 = ["bunny-primary-640x480", "conference-ao-640x480", "sponza-diffuse-640x480", "sponza-diffuse2-640x480"]
 
 
+# PMC-measured HBM traffic per launch (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in
+# separate passes, tools/profile_round.sh + tools/summarize_prof.py); counters
+# cannot be read inside this timed process, so the committed profile is cited.
+PMC_PROFILES = {"bunny-primary-1024x768": "profiles/round1_bunny1024_pmc_summary.json"}
+
+
+def pmc_traffic(name):
+    path = os.path.join(REPO, PMC_PROFILES.get(name, "-"))
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        s = json.load(f)
+    hbm = s.get("hbm_bytes_per_launch")
+    return (int(hbm["total_corrected"]) if hbm else None), PMC_PROFILES[name]
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -260,7 +276,8 @@ def run_workload(name, tracer, world, rank, steps, warmup, exact, want_cpu):
                     "leaves": round(n_leaves / batches.rays_traced, 2),
                     "bytes": round(alg_bytes / batches.rays_traced, 1)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(name)[0],
+                     "traffic_source": pmc_traffic(name)[1],
                      "algorithmic_bytes_per_launch": int(alg_bytes / len(batches.batches))},
         "reference_mrays": REFERENCE_MRAYS.get(name),
     }
