@@ -76,15 +76,15 @@ struct DeviceGuard {
 mrt_launch_cfg default_cfg() {
     mrt_launch_cfg c;
     c.waves_per_cu = 0;   // auto: sized from the batch (grid_blocks)
-    c.fetch_threshold = 40;
-    c.num_queues = 8;
+    c.fetch_threshold = 0;   // strided mode: a wave refills once all its lanes are done
+    c.num_queues = -1;       // static strided assignment (see trace_kernel.hip); 1..8 = atomic queues
     c.lds_stack = 16;
     return c;
 }
 
 bool valid_cfg(const mrt_launch_cfg& c) {
     return (c.waves_per_cu == 0 || (c.waves_per_cu >= 4 && c.waves_per_cu <= 32)) && c.fetch_threshold >= 0 && c.fetch_threshold <= 64 &&
-           c.num_queues >= 1 && c.num_queues <= mrt::kMaxQueues &&
+           (c.num_queues == -1 || (c.num_queues >= 1 && c.num_queues <= mrt::kMaxQueues)) &&
            (c.lds_stack == 8 || c.lds_stack == 16 || c.lds_stack == 32);
 }
 
@@ -101,10 +101,12 @@ mrt::TraceVariant variant_for(const mrt_tracer* t, uint32_t flags) {
 // Rays per lane the automatic grid aims for: a frame-sized batch is bound by
 // its slowest rays, whose step latency grows with the number of co-resident
 // waves, so small batches get fewer waves per CU; big batches fill the CU.
-// Measured on MI355X (tools/sweep.py, profiles/round1_sweep.txt): 8 waves/CU
-// is best up to ~1M rays (bunny primary 1024x768, conference AO), 16 at 3M,
-// 32 at 12M rays.
+// Measured on MI355X (tools/sweep.py, profiles/round1_sweep.txt): batches that
+// fit one ray per lane at 32 waves/CU run fastest fully static (conference AO
+// 640x480: 0.061 ms vs 0.077 at 8 waves); above that, 8 waves/CU is best up to
+// ~1M rays (bunny primary 1024x768), 16 at 3M, 32 at 12M rays.
 constexpr int kAutoRaysPerLane = 12;
+constexpr int kStridedWaves = 28;
 constexpr int kAutoMinWaves = 8;
 
 // Persistent grid: as many 256-thread workgroups per CU as the config asks for
@@ -114,9 +116,20 @@ int grid_blocks(const mrt_tracer* t, const mrt::TraceVariant& v, int numRays, in
     int occ = 0;
     if (mrt::trace_occupancy(v, &occ) != hipSuccess || occ <= 0) occ = 1;
     int waves = t->cfg.waves_per_cu;
-    if (waves == 0) {
-        const long long lanesPerCU = (long long)numRays / kAutoRaysPerLane / std::max(1, t->numCUs);
-        waves = (int)std::min<long long>(32, std::max<long long>(kAutoMinWaves, (lanesPerCU + 63) / 64));
+    if (waves == 0 && t->cfg.num_queues < 0) {
+        // Static strided assignment: 28 waves/CU (7 workgroups) measured best or
+        // within 2 % of best from 307k to 12.6M rays (profiles/round1_sweep.txt).
+        waves = kStridedWaves;
+    } else if (waves == 0) {
+        const long long cus = std::max(1, t->numCUs);
+        if ((long long)numRays <= 32LL * 64 * cus) {
+            // The whole batch fits the first (static, atomic-free) round at full
+            // occupancy: one ray per lane, no dynamic fetch at all.
+            waves = 32;
+        } else {
+            const long long lanesPerCU = (long long)numRays / kAutoRaysPerLane / cus;
+            waves = (int)std::min<long long>(32, std::max<long long>(kAutoMinWaves, (lanesPerCU + 63) / 64));
+        }
     }
     const int want = std::max(1, (waves + 3) / (mrt::kBlockThreads / 64));
     const int perCU = std::min(want, occ);
@@ -173,7 +186,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     a.nodeBytes = (uint32_t)t->nodeBytes;
     a.woopBytes = (uint32_t)t->woopBytes;
     a.numRays = numRays;
-    a.numQueues = std::min(t->cfg.num_queues, std::max(1, numRays));
+    a.numQueues = t->cfg.num_queues < 0 ? 0 : std::min(t->cfg.num_queues, std::max(1, numRays));
     a.fetchThreshold = t->cfg.fetch_threshold;
     a.totalLanes = totalLanes;
     a.queues = t->queues;

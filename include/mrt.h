@@ -62,9 +62,10 @@ typedef struct mrt_tracer mrt_tracer;   /* one per HIP device; re-entrant per ha
 /* Tuning knobs of the persistent launch (0 = library default). */
 typedef struct mrt_launch_cfg {
     int32_t waves_per_cu;      /* persistent waves per CU (grid = CUs * waves_per_cu); 0 = auto (by batch size) */
-    int32_t fetch_threshold;   /* refill a wave when fewer than this many of its 64 lanes are live
+    int32_t fetch_threshold;   /* refill a wave when fewer than this many of its 64 lanes are live (0 = when all are done)
                                   (reference DYNAMIC_FETCH_THRESHOLD 20 of 32, kepler_dynamic_fetch.cu:48) */
-    int32_t num_queues;        /* ray work queues (1..8); default 8 = one per XCD                 */
+    int32_t num_queues;        /* ray work queues (1..8, default 8 = one per XCD); -1 = static strided
+                                  assignment (lane L takes rays L, L+T, ...; no atomics)           */
     int32_t lds_stack;         /* traversal-stack entries per lane kept in LDS: 8, 16 or 32       */
 } mrt_launch_cfg;
 

@@ -158,7 +158,9 @@ def test_fast_rcp_within_tolerance(tracer, wl):
 
 # ---------------------------------------------------------------- launch configs
 @pytest.mark.parametrize("cfg", [dict(lds_stack=8), dict(lds_stack=32), dict(waves_per_cu=8),
-                                 dict(num_queues=1), dict(fetch_threshold=0), dict(fetch_threshold=64),
+                                 dict(num_queues=1), dict(num_queues=8, fetch_threshold=40),
+                                 dict(num_queues=8, waves_per_cu=32, fetch_threshold=64),
+                                 dict(num_queues=-1, fetch_threshold=16), dict(num_queues=-1, waves_per_cu=4),
                                  dict(waves_per_cu=4, lds_stack=8, num_queues=3)],
                          ids=lambda c: ",".join(f"{k}={v}" for k, v in c.items()))
 def test_launch_configs_do_not_change_results(tracer, cfg):
