@@ -192,30 +192,30 @@ def algorithmic_bytes(tracer, batches):
 
 def time_steps(tracer, batches, steps, warmup, world, exact):
     """Warmup, then exactly `steps` steps bracketed by barrier + synchronize.
-    Per-launch HIP events on the launch stream give the kernel duration."""
+    One HIP event pair on the launch stream around the K steps gives the GPU
+    time per launch (kernel duration plus the inter-launch gap, an upper bound on
+    the kernel's own average); no per-launch host work besides the launch."""
     import torch
     stream = torch.cuda.current_stream()
+    launches = [tracer.launcher(rb, exact_rcp=exact, stream=stream) for rb, _ in batches.batches]
     for _ in range(warmup):
-        for rb, _ in batches.batches:
-            tracer.trace_async(rb, exact_rcp=exact, stream=stream)
-    nb = len(batches.batches)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps * nb)]
+        for go in launches:
+            go()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    k = 0
+    e0.record(stream)
     for _ in range(steps):
-        for rb, _ in batches.batches:
-            ev[k][0].record(stream)
-            tracer.trace_async(rb, exact_rcp=exact, stream=stream)
-            ev[k][1].record(stream)
-            k += 1
+        for go in launches:
+            go()
+    e1.record(stream)
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    launch_ms = e0.elapsed_time(e1) / (steps * len(launches))
     return wall, launch_ms
 
 
@@ -302,6 +302,8 @@ def main():
     ap.add_argument("--fetch-threshold", type=int, default=-1)
     ap.add_argument("--lds-stack", type=int, default=0)
     ap.add_argument("--queues", type=int, default=0)
+    ap.add_argument("--node-levels", type=int, default=0)
+    ap.add_argument("--lane-groups", type=int, default=0)
     args = ap.parse_args()
 
     import torch
@@ -318,6 +320,10 @@ def main():
         cfg["lds_stack"] = args.lds_stack
     if args.queues:
         cfg["num_queues"] = args.queues
+    if args.node_levels:
+        cfg["node_levels"] = args.node_levels
+    if args.lane_groups:
+        cfg["lane_groups"] = args.lane_groups
     if cfg:
         tracer.set_config(**cfg)
     exact = args.rcp == "exact"

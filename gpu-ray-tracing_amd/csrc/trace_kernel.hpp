@@ -23,13 +23,16 @@ struct TraceArgs {
     const float4* rays;        // Ray[n] as 2 x float4
     int2* results;             // RayResult[n] viewed as int2 pairs; slot 2*i = {id, t}
     const float4* nodes;       // Compact2 nodes
+    const float4* treelets;    // treelet records (TREELET variants), 4 x nodeBytes
     const float4* woop;        // Woop triangles
     const int* triIndex;       // remap table
     uint32_t nodeBytes;        // buffer-resource ranges (range-checked loads)
     uint32_t woopBytes;
+    uint32_t treeletBytes;
     int numRays;
     int numQueues;             // 1..8 ray queues (per-XCD heads)
     int fetchThreshold;        // refill when fewer live lanes than this
+    int laneGroupsLog2;        // strided mode: a wave's lanes take rays from 2^k spread-out sub-ranges
     int totalLanes;            // grid lanes (stride of the spill slab)
     unsigned* queues;          // numQueues heads, kQueueStrideWords apart, zeroed per launch
     int* spill;                // (kStackCapacity - S) * totalLanes ints
@@ -44,7 +47,11 @@ struct TraceVariant {
     bool exactRcp;      // IEEE 1/x vs v_rcp_f32
     bool stats;
     int ldsStack;       // 8, 16 or 32 LDS entries per lane
+    bool treelet;       // fetch node + both children per round trip (treelet records)
 };
+
+// Treelet records for the bound BVH: records must hold 4 * nodeBytes bytes.
+hipError_t build_treelets(const void* nodes, uint64_t nodeBytes, void* records, hipStream_t s);
 
 // Launch one persistent trace. grid = number of 256-thread workgroups.
 hipError_t launch_trace(const TraceVariant& v, const TraceArgs& a, int gridBlocks, hipStream_t s);

@@ -143,6 +143,22 @@ class Tracer:
         _lib.check(self.lib.mrt_tracer_trace(self._h, rays.rays.data_ptr(), rays.results.data_ptr(), rays.size, f,
                                              sp, _stream_ptr(stream)))
 
+    def launcher(self, rays: RayBuffer, exact_rcp=False, speculative=True, stream=None):
+        """A zero-argument callable that re-issues trace_async(rays, ...) with every
+        argument resolved once: one C call per launch, for tight launch loops."""
+        if self.bvh is None:
+            raise _lib.MrtError("Tracer: No BVH!")
+        fn, h = self.lib.mrt_tracer_trace, self._h
+        args = (rays.rays.data_ptr(), rays.results.data_ptr(), rays.size, self.flags(rays, exact_rcp, speculative),
+                None, _stream_ptr(stream))
+        check = _lib.check
+
+        def launch():
+            rc = fn(h, *args)
+            if rc:
+                check(rc)
+        return launch
+
     def trace_batch(self, rays: RayBuffer, exact_rcp=False, speculative=True, stats=False, stream=None) -> float:
         """CudaTracer::traceBatch: blocking, returns the launch's milliseconds (0 for no rays)."""
         if self.bvh is None:

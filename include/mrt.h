@@ -67,6 +67,12 @@ typedef struct mrt_launch_cfg {
     int32_t num_queues;        /* ray work queues (1..8, default 8 = one per XCD); -1 = static strided
                                   assignment (lane L takes rays L, L+T, ...; no atomics)           */
     int32_t lds_stack;         /* traversal-stack entries per lane kept in LDS: 8, 16 or 32       */
+    int32_t node_levels;       /* binary BVH levels per node fetch: 1 = one Compact2 node; 2 = the node
+                                  and both children's nodes in one 256-B treelet record (library-owned,
+                                  4 x nodeBytes, built from the bound nodes on first use; needs
+                                  nodeBytes < 1 GiB, else 1 is used). Same visit order and results. */
+    int32_t lane_groups;       /* strided mode: a wave's 64 lanes take rays from this many (1..64, power of
+                                  two) distant sub-ranges of the batch instead of 64 consecutive rays */
 } mrt_launch_cfg;
 
 /* Per-launch statistics reported back to the host (optional). */
@@ -76,6 +82,7 @@ typedef struct mrt_trace_info {
     int32_t block_threads;     /* threads per workgroup                                           */
     int32_t lds_stack_entries; /* per-lane traversal-stack entries held in LDS                    */
     int32_t stack_overflows;   /* lanes that needed more than 64 stack entries (0 for SBVH depth<=64) */
+    int32_t node_levels;       /* binary levels per node fetch the launch used (1 or 2)           */
 } mrt_trace_info;
 
 /* ---- handle API -------------------------------------------------------- */

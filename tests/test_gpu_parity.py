@@ -161,7 +161,10 @@ def test_fast_rcp_within_tolerance(tracer, wl):
                                  dict(num_queues=1), dict(num_queues=8, fetch_threshold=40),
                                  dict(num_queues=8, waves_per_cu=32, fetch_threshold=64),
                                  dict(num_queues=-1, fetch_threshold=16), dict(num_queues=-1, waves_per_cu=4),
-                                 dict(waves_per_cu=4, lds_stack=8, num_queues=3)],
+                                 dict(waves_per_cu=4, lds_stack=8, num_queues=3), dict(node_levels=1),
+                                 dict(node_levels=2, lds_stack=8, num_queues=3),
+                                 dict(node_levels=2, lds_stack=32, waves_per_cu=4), dict(lane_groups=2),
+                                 dict(lane_groups=8), dict(lane_groups=64, waves_per_cu=4)],
                          ids=lambda c: ",".join(f"{k}={v}" for k, v in c.items()))
 def test_launch_configs_do_not_change_results(tracer, cfg):
     bufs, rays, any_hit, want, st = scene_setup("conference", 256, 192, "diffuse")
@@ -176,12 +179,45 @@ def test_launch_configs_do_not_change_results(tracer, cfg):
         tracer.set_config(**saved)
 
 
+@pytest.mark.parametrize("wl", WORKLOADS, ids=lambda w: "-".join(map(str, w)))
+def test_treelet_fetch_is_bit_identical(tracer, wl):
+    """node_levels=2 (node + both children per round trip) visits the same nodes
+    in the same order: results and per-ray counters equal the oracle's."""
+    bufs, rays, any_hit, want, st = scene_setup(*wl)
+    saved = tracer.config()
+    for levels in (1, 2):
+        try:
+            tracer.set_config(node_levels=levels)
+            res, gst = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=False, stats=True)
+            assert tracer.last_info["node_levels"] == levels
+            assert np.array_equal(res[:, :2], want[:, :2]) and np.array_equal(gst[:, :3], st[:, :3])
+            res2, _ = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=True)
+            if any_hit:
+                assert_valid_hits(rays, res2, want, bufs)
+            else:
+                assert np.array_equal(res2[:, :2], want[:, :2])
+        finally:
+            tracer.set_config(**saved)
+
+
+def test_treelets_follow_rebinding(tracer):
+    """The treelet records are rebuilt from whatever BVH is bound last."""
+    saved = tracer.config()
+    try:
+        tracer.set_config(node_levels=2)
+        test_rebinding_a_different_bvh(tracer)
+    finally:
+        tracer.set_config(**saved)
+
+
 def test_invalid_config_rejected(tracer):
     from mrt._lib import MrtError
     with pytest.raises(MrtError):
         tracer.set_config(lds_stack=12)
     with pytest.raises(MrtError):
         tracer.set_config(num_queues=9)
+    with pytest.raises(MrtError):
+        tracer.set_config(node_levels=3)
 
 
 # ---------------------------------------------------------------- edge cases
