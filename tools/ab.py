@@ -1,0 +1,108 @@
+"""Interleaved A/B timing of trace variants on one box, in one process.
+
+A variant is (library directory, launch config): each library copy is loaded
+RTLD_LOCAL under its own handle, so two builds of libmrt.so (e.g. the current
+tree and a saved one) can be compared on the same GPU, same clocks, same
+inputs. Rounds alternate the variants; the median per-launch time is printed.
+
+  python tools/ab.py --workload bunny-primary-1024x768 \
+      --variant lib:'{}' --variant /tmp/libB:'{"waves_per_cu": 24}'
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "gpu-ray-tracing_amd"))
+
+
+def load(libdir):
+    from mrt import _lib
+    path = os.path.join(libdir if os.path.isabs(libdir) else os.path.join(REPO, "gpu-ray-tracing_amd", libdir),
+                        "libmrt.so")
+    # Two copies of the library in one process must each bind to their own
+    # definitions (mrt::launch_trace & co.), or one copy's glue would launch
+    # the other's kernels with a different argument layout.
+    import subprocess
+    dyn = subprocess.run(["readelf", "-d", path], capture_output=True, text=True).stdout
+    if "SYMBOLIC" not in dyn:
+        raise SystemExit(f"{path} is not linked -Bsymbolic; refusing to load it next to another copy")
+    lib = C.CDLL(path, mode=C.RTLD_LOCAL)
+    for name, res, args in _lib.TRACE_SYMBOLS:
+        fn = getattr(lib, name)
+        fn.restype, fn.argtypes = res, args
+    return lib
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="bunny-primary-1024x768")
+    ap.add_argument("--variant", action="append", required=True, help="libdir:json-config")
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--launches", type=int, default=20)
+    ap.add_argument("--fast-rcp", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import bench
+    from mrt import _lib
+    from mrt.tracer import Tracer
+    torch.cuda.set_device(0)
+    scene_name = bench.workload_spec(args.workload)[0]
+    scene, bufs, _, _ = bench.bvh_for(scene_name, 1, 0)
+    b = bench.Batches(args.workload, scene, bufs, Tracer(0))
+    g = b.gbvh
+    stream = torch.cuda.current_stream()
+    variants = []
+    for spec in args.variant:
+        libdir, cfg = spec.split(":", 1)
+        lib = load(libdir)
+        h = C.c_void_p()
+        assert lib.mrt_tracer_create(0, C.byref(h)) == 0
+        assert lib.mrt_tracer_bind(h, g.nodes.data_ptr(), g.node_bytes, g.woop.data_ptr(), g.woop_bytes,
+                                   g.tri_index.data_ptr(), g.tri_index_bytes) == 0
+        c = _lib.LaunchCfg()
+        assert lib.mrt_tracer_get_config(h, C.byref(c)) == 0
+        for k, v in json.loads(cfg or "{}").items():
+            setattr(c, k, v)
+        rc = lib.mrt_tracer_set_config(h, C.byref(c))
+        assert rc == 0, f"config {cfg} rejected"
+        variants.append((spec, lib, h))
+    ref = None
+    times = {spec: [] for spec, _, _ in variants}
+    for r in range(args.rounds + 1):
+        for spec, lib, h in variants:
+            launches = []
+            for rb, _ in b.batches:
+                flags = (0 if rb.need_closest_hit else _lib.MRT_TRACE_ANY_HIT) | (0 if args.fast_rcp else _lib.MRT_TRACE_EXACT_RCP)
+                launches.append((rb.rays.data_ptr(), rb.results.data_ptr(), rb.size, flags))
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record(stream)
+            for _ in range(args.launches):
+                for rp, res, n, fl in launches:
+                    lib.mrt_tracer_trace(h, rp, res, n, fl, None, stream.cuda_stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            if r > 0:
+                times[spec].append(e0.elapsed_time(e1) / (args.launches * len(launches)))
+            out = b.batches[-1][0].results_numpy()[:, :2].copy()
+            if ref is None:
+                ref = out
+            elif b.batches[-1][0].need_closest_hit and not np.array_equal(out, ref):
+                print(f"  WARNING: {spec} results differ from the first variant", flush=True)
+    base = np.median(times[variants[0][0]])
+    print(f"{args.workload} ({b.rays_traced} rays/step):")
+    for spec, _, _ in variants:
+        m = np.median(times[spec])
+        print(f"  {spec:60s} median {m:.4f} ms  min {min(times[spec]):.4f}  max {max(times[spec]):.4f}  "
+              f"x{base / m:.3f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
