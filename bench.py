@@ -138,38 +138,42 @@ def bvh_for(scene_name, world, rank):
 
 
 class Batches:
-    """Ray batches of one workload, generated on the host exactly like the
-    reference Renderer (Renderer.cc:112-152,242-291): primary rays in Morton
-    order; AO/diffuse rays from the primary hits (degenerate tmax=-1 rays for
-    misses are traced too; only primary hits are counted)."""
+    """Ray batches of one workload, generated on the device like the reference
+    Renderer (Renderer.cc:112-152,242-291; RayGen.cc:50-120): primary rays in
+    Morton order; AO/diffuse rays from the traced primary hits (degenerate
+    tmax=-1 rays for misses are traced too; only primary hits are counted)."""
 
     def __init__(self, name, scene, bufs, tracer):
-        import mrt
-        from mrt.tracer import GpuBvh, RayBuffer
+        from mrt.raygen import DeviceRayGen
+        from mrt.tracer import GpuBvh
         sname, w, h, kind, bounces = workload_spec(name)
         self.name, self.kind, self.w, self.h = name, kind, w, h
         self.gbvh = GpuBvh(bufs)
         tracer.set_bvh(self.gbvh)
         cam, ao_radius = scene.camera()
-        rays, _ = mrt.primary_rays(cam, w, h)
+        gen = DeviceRayGen(scene)   # RayGen on the device (mrt_raygen_*), like the reference's RayGenKernels
+        prim, _ = gen.primary(cam, w, h)
         self.batches = []   # (RayBuffer, rays counted)
         if kind == "primary":
-            self.batches.append((RayBuffer(rays, need_closest_hit=True), w * h))
+            self.batches.append((prim, w * h))
         else:
-            prev = RayBuffer(rays, need_closest_hit=True)
-            tracer.trace_batch(prev, exact_rcp=True)
-            prev_rays, prev_res = rays, prev.results_numpy()
+            tracer.trace_batch(prim, exact_rcp=True)
+            prev = prim
             for b in range(bounces):
-                hits = mrt.count_hits(prev_res)
+                hits = gen.count_hits(prev)
                 max_dist = ao_radius if kind == "ao" else cam.far
-                sec = mrt.ao_rays(prev_rays, prev_res, scene, max_dist, 1, mrt.AO_SEED + b)
-                rb = RayBuffer(sec, need_closest_hit=(kind == "diffuse"))
+                rb = gen.ao(prev, 1, max_dist, mrt_seed(b), closest_hit=(kind == "diffuse"))
                 self.batches.append((rb, hits))
                 if b + 1 < bounces:
                     tracer.trace_batch(rb, exact_rcp=True)
-                    prev_rays, prev_res = sec, rb.results_numpy()
+                    prev = rb
         self.rays_counted = sum(c for _, c in self.batches)
         self.rays_traced = sum(rb.size for rb, _ in self.batches)
+
+
+def mrt_seed(bounce):
+    import mrt
+    return mrt.AO_SEED + bounce
 
 
 def algorithmic_bytes(tracer, batches):
@@ -353,7 +357,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": round(head["value"] / ref, 3) if ref else None,
             "dtype": "f32",
-            "data": "synthetic (deterministic stand-in scene with the README triangle count; host-generated rays)",
+            "data": "synthetic (deterministic stand-in scene with the README triangle count; rays generated on the device)",
             "config": {"workload": args.workload, "scene": workload_spec(args.workload)[0],
                        "scene_tris": head["scene_tris"], "width": workload_spec(args.workload)[1],
                        "height": workload_spec(args.workload)[2], "ray_type": workload_spec(args.workload)[3],

@@ -204,8 +204,7 @@ int mrth_pixel_table(int32_t w, int32_t h, int32_t* indexToPixel) {
     return MRTH_OK;
 }
 
-int mrth_primary_rays(const mrth_camera* cam, int32_t w, int32_t h, void* rays, int32_t* slotToId) {
-    if (!cam || w <= 0 || h <= 0 || !rays) return fail(MRTH_ERR_INVALID_ARG, "bad arguments");
+static mrt::Camera to_camera(const mrth_camera* cam) {
     mrt::Camera c;
     c.position = v3(cam->position);
     c.forward = v3(cam->forward);
@@ -213,7 +212,19 @@ int mrth_primary_rays(const mrth_camera* cam, int32_t w, int32_t h, void* rays, 
     c.fov = cam->fov_deg;
     c.nearDist = cam->near_dist;
     c.farDist = cam->far_dist;
-    mrt::gen_primary_rays(c, w, h, static_cast<mrt::Ray*>(rays), slotToId);
+    return c;
+}
+
+int mrth_primary_rays(const mrth_camera* cam, int32_t w, int32_t h, void* rays, int32_t* slotToId) {
+    if (!cam || w <= 0 || h <= 0 || !rays) return fail(MRTH_ERR_INVALID_ARG, "bad arguments");
+    mrt::gen_primary_rays(to_camera(cam), w, h, static_cast<mrt::Ray*>(rays), slotToId);
+    return MRTH_OK;
+}
+
+int mrth_camera_nscreen_to_world(const mrth_camera* cam, int32_t w, int32_t h, float out[16]) {
+    if (!cam || w <= 0 || h <= 0 || !out) return fail(MRTH_ERR_INVALID_ARG, "bad arguments");
+    const mrt::Mat4f m = mrt::nscreen_to_world(to_camera(cam), w, h);
+    for (int i = 0; i < 16; i++) out[i] = m.m[i];
     return MRTH_OK;
 }
 

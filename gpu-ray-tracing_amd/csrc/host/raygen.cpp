@@ -2,7 +2,9 @@
 // primary / AO / diffuse ray generators, on the host.
 //
 // Restates (with IEEE host arithmetic instead of the reference's
-// --use_fast_math device code, so results agree statistically, not bitwise):
+// --use_fast_math device code, so results agree statistically, not bitwise;
+// the per-ray arithmetic lives in ../raygen_common.hpp, shared with the gfx950
+// generators of csrc/raygen_kernel.hip):
 //   camera      CameraControls::getOrientation/getWorldToCamera (CameraControls.cc:263-296),
 //               Mat4f::perspective / fitToView (Math.cc:66-93),
 //               nscreenToWorld = invert(fitToView(-1, 2, size) * worldToClip) (Renderer.cc:126-129)
@@ -14,10 +16,12 @@
 //               angle per ray, tmax = -1 for primary misses (degenerate rays)
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <thread>
 #include <vector>
 
 #include "raygen.hpp"
+#include "../raygen_common.hpp"
 
 namespace mrt {
 
@@ -52,18 +56,6 @@ Mat4f fit_to_view(float w, float h) {   // Math.cc:66-75 with pos = -1, size = 2
     const float s = fw_min(w / 2.0f, h / 2.0f);
     return Mat4f::scale(Vec3f(2.0f / w, 2.0f / h, 1.0f)) * Mat4f::scale(Vec3f(s, s, 1.0f)) *
            Mat4f::translate(Vec3f(0.0f, 0.0f, 0.0f));
-}
-
-inline void jenkins_mix(uint32_t& a, uint32_t& b, uint32_t& c) {   // RayGenKernels.cu:36-47
-    a -= b; a -= c; a ^= (c >> 13);
-    b -= c; b -= a; b ^= (a << 8);
-    c -= a; c -= b; c ^= (b >> 13);
-    a -= b; a -= c; a ^= (c >> 12);
-    b -= c; b -= a; b ^= (a << 16);
-    c -= a; c -= b; c ^= (b >> 5);
-    a -= b; a -= c; a ^= (c >> 3);
-    b -= c; b -= a; b ^= (a << 10);
-    c -= a; c -= b; c ^= (b >> 15);
 }
 
 template <class F>
@@ -127,17 +119,12 @@ std::vector<int32_t> pixel_table(int w, int h) {   // PixelTable.cc:70-161 ("sma
 void gen_primary_rays(const Camera& cam, int w, int h, Ray* out, int32_t* slotToId) {
     const Mat4f m = nscreen_to_world(cam, w, h);
     const std::vector<int32_t> table = pixel_table(w, h);
+    const rg::V3 origin = rg::make(cam.position.x, cam.position.y, cam.position.z);
     parallel_for((int64_t)w * h, [&](int64_t lo, int64_t hi) {
         for (int64_t task = lo; task < hi; task++) {
             const int pixel = table[task];
-            const Vec4f ns(2.0f * ((float)(pixel % w) + 0.5f) / (float)w - 1.0f,
-                           2.0f * ((float)(pixel / w) + 0.5f) / (float)h - 1.0f, 0.0f, 1.0f);
-            const Vec4f wp4 = m * ns;
-            const Vec3f wp = Vec3f(wp4.x, wp4.y, wp4.z) / wp4.w;
-            const Vec3f dir = normalize(wp - cam.position);
-            Ray& r = out[task];
-            r.ox = cam.position.x; r.oy = cam.position.y; r.oz = cam.position.z; r.tmin = 0.0f;
-            r.dx = dir.x; r.dy = dir.y; r.dz = dir.z; r.tmax = cam.farDist;
+            const rg::RayRec r = rg::primary_ray(m.m, origin, cam.farDist, w, h, pixel);
+            std::memcpy(&out[task], &r, sizeof(Ray));
             if (slotToId) slotToId[task] = pixel;
         }
     });
@@ -145,55 +132,17 @@ void gen_primary_rays(const Camera& cam, int w, int h, Ray* out, int32_t* slotTo
 
 void gen_ao_rays(const Ray* inRays, const RayResult* inResults, int64_t numInput, const Vec3f* triNormals,
                  int64_t numTris, int numSamples, float maxDist, uint32_t seed, Ray* out) {
+    static_assert(sizeof(Vec3f) == 12, "normals are packed float triples");
+    const float* normals = reinterpret_cast<const float*>(triNormals);
     parallel_for(numInput, [&](int64_t lo, int64_t hi) {
         for (int64_t task = lo; task < hi; task++) {
-            const Ray& ir = inRays[task];
-            const RayResult& res = inResults[task];
-            const Vec3f o(ir.ox, ir.oy, ir.oz), d(ir.dx, ir.dy, ir.dz);
-            const Vec3f origin = o + d * fw_max(res.t - 1.0e-4f, 0.0f);
-
-            const int tri = res.id;
-            Vec3f normal(1.0f, 0.0f, 0.0f);
-            if (tri >= 0 && tri < numTris) normal = triNormals[tri];
-            if (dot(normal, d) > 0.0f) normal = -normal;
-
-            const Vec3f na = vabs(normal);
-            const float nm = fw_max(fw_max(na.x, na.y), na.z);
-            Vec3f perp(normal.y, -normal.x, 0.0f);
-            if (nm == na.z) perp = Vec3f(0.0f, normal.z, -normal.y);
-            else if (nm == na.x) perp = Vec3f(-normal.z, 0.0f, normal.x);
-            perp = normalize(perp);
-            const Vec3f biperp = cross(normal, perp);
-
-            uint32_t ha = seed + (uint32_t)task, hb = 0x9e3779b9u, hc = 0x9e3779b9u;
-            jenkins_mix(ha, hb, hc);
-            jenkins_mix(ha, hb, hc);
-            const float angle = 2.0f * kPiF * (float)hc * 0x1p-32f;
-            const float ca = std::cos(angle), sa = std::sin(angle);
-            const Vec3f t0 = perp * ca + biperp * sa;
-            const Vec3f t1 = perp * -sa + biperp * ca;
-
+            rg::RayRec in;
+            std::memcpy(&in, &inRays[task], sizeof(in));
+            const rg::AOBasis b =
+                rg::ao_basis(in, inResults[task].id, inResults[task].t, normals, numTris, seed, (uint32_t)task);
             for (int i = 0; i < numSamples; i++) {
-                float x = 0.0f, xadd = 1.0f;
-                for (unsigned hc2 = (unsigned)i + 1; hc2 != 0; hc2 >>= 1) {
-                    xadd *= 0.5f;
-                    if (hc2 & 1) x += xadd;
-                }
-                float y = 0.0f, yadd = 1.0f;
-                for (int hc3 = i + 1; hc3 != 0; hc3 /= 3) {
-                    yadd *= 1.0f / 3.0f;
-                    y += (float)(hc3 % 3) * yadd;
-                }
-                const float a2 = 2.0f * kPiF * y;
-                const float r = std::sqrt(x);
-                x = r * std::cos(a2);
-                y = r * std::sin(a2);
-                const float z = std::sqrt(1.0f - x * x - y * y);
-                const Vec3f dir = normalize(t0 * x + t1 * y + normal * z);
-                Ray& orr = out[task * numSamples + i];
-                orr.ox = origin.x; orr.oy = origin.y; orr.oz = origin.z; orr.tmin = 0.0f;
-                orr.dx = dir.x; orr.dy = dir.y; orr.dz = dir.z;
-                orr.tmax = (tri == -1) ? -1.0f : maxDist;
+                const rg::RayRec r = rg::ao_sample(b, i, maxDist);
+                std::memcpy(&out[task * numSamples + i], &r, sizeof(Ray));
             }
         }
     });
@@ -201,7 +150,7 @@ void gen_ao_rays(const Ray* inRays, const RayResult* inResults, int64_t numInput
 
 int64_t count_hits(const RayResult* results, int64_t n) {   // countHitsKernel (RendererKernels.cu:114-162)
     int64_t hits = 0;
-    for (int64_t i = 0; i < n; i++) hits += (results[i].id != -1);
+    for (int64_t i = 0; i < n; i++) hits += (results[i].id >= 0);
     return hits;
 }
 

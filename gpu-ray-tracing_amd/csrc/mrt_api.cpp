@@ -50,14 +50,22 @@ struct mrt_tracer {
     bool treeletsValid = false;
 };
 
+namespace mrt {
 namespace {
-
 thread_local std::string g_lastError;
+}  // namespace
 
-int fail(int code, const std::string& what) {
+// Shared with the ray-generation entry points (csrc/raygen_kernel.hip).
+int api_fail(int code, const std::string& what) {
     g_lastError = what;
     return code;
 }
+const char* api_last_error() { return g_lastError.c_str(); }
+}  // namespace mrt
+
+namespace {
+
+int fail(int code, const std::string& what) { return mrt::api_fail(code, what); }
 
 int hipFail(hipError_t e, const char* what) {
     return fail(MRT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -300,7 +308,7 @@ const char* mrt_error_string(int err) {
     }
 }
 
-const char* mrt_last_error_detail(void) { return g_lastError.c_str(); }
+const char* mrt_last_error_detail(void) { return mrt::api_last_error(); }
 
 int mrt_device_count(void) {
     int n = 0;

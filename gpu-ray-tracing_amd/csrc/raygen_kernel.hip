@@ -1,0 +1,185 @@
+// raygen_kernel.hip — the trace's producers and consumer on the device (gfx950):
+// primary rays, AO/diffuse hemisphere rays and the hit count, so a frame
+// (primary -> trace -> AO -> trace) never leaves HBM.
+//
+//   mrt_raygen_primary  <- RayGen::primary + rayGenPrimaryKernel (reference RayGen.cc:50-72,
+//                          RayGenKernels.cu:79-113)
+//   mrt_raygen_ao       <- RayGen::ao + rayGenAOKernel (RayGen.cc:77-120, RayGenKernels.cu:117-227)
+//   mrt_count_hits      <- countHitsKernel / launch_countHitsKernel (RendererKernels.cu:112-162,189-)
+//
+// The per-ray arithmetic is csrc/raygen_common.hpp, the same code the host
+// generator runs. These are streaming kernels (32 B written per ray, 16-48 B
+// read): one thread per output ray, 256-thread blocks, no LDS. The hit count
+// is a shuffle reduction, one partial per block and a one-block final sum (no
+// contended atomics).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/mrt.h"
+#include "raygen_common.hpp"
+#include "trace_kernel.hpp"
+
+namespace mrt {
+namespace {
+
+constexpr int kThreads = 256;
+
+struct PrimaryArgs {
+    float m[16];   // column-major nscreen-to-world
+    float ox, oy, oz, maxDist;
+    int w, h;
+    const int32_t* indexToPixel;
+    rg::RayRec* rays;
+    int32_t* slotToId;
+    int32_t* idToSlot;
+};
+
+__global__ __launch_bounds__(kThreads) void primary_kernel(PrimaryArgs a) {
+    const int task = (int)(blockIdx.x * kThreads + threadIdx.x);
+    if (task >= a.w * a.h) return;
+    const int pixel = a.indexToPixel[task];
+    a.rays[task] = rg::primary_ray(a.m, rg::make(a.ox, a.oy, a.oz), a.maxDist, a.w, a.h, pixel);
+    if (a.slotToId) a.slotToId[task] = pixel;
+    if (a.idToSlot) a.idToSlot[pixel] = task;
+}
+
+struct AOArgs {
+    const rg::RayRec* inRays;
+    const int2* inResults;   // RayResult viewed as int2 pairs: slot 2*i = {id, t bits}
+    int numInput;
+    const float* normals;
+    int64_t numTris;
+    int numSamples;
+    float maxDist;
+    uint32_t seed;
+    rg::RayRec* outRays;
+    int32_t* outIdToSlot;
+    int32_t* outSlotToId;
+};
+
+__global__ __launch_bounds__(kThreads) void ao_kernel(AOArgs a) {
+    const int task = (int)(blockIdx.x * kThreads + threadIdx.x);
+    if (task >= a.numInput) return;
+    const int2 res = a.inResults[2 * task];
+    const rg::AOBasis b =
+        rg::ao_basis(a.inRays[task], res.x, __int_as_float(res.y), a.normals, a.numTris, a.seed, (uint32_t)task);
+    const int64_t out = (int64_t)task * a.numSamples;
+    for (int i = 0; i < a.numSamples; i++) {
+        a.outRays[out + i] = rg::ao_sample(b, i, a.maxDist);
+        if (a.outIdToSlot) a.outIdToSlot[out + i] = (int32_t)(out + i);
+        if (a.outSlotToId) a.outSlotToId[out + i] = (int32_t)(out + i);
+    }
+}
+
+// Per block: hits among its rays (id >= 0, RendererKernels.cu:131), one partial.
+__global__ __launch_bounds__(kThreads) void count_partial_kernel(const int4* results, int n, int perBlock,
+                                                                int32_t* partial) {
+    __shared__ int waveSum[kThreads / 64];
+    const int begin = (int)blockIdx.x * perBlock;
+    const int end = min(begin + perBlock, n);
+    int c = 0;
+    for (int i = begin + (int)threadIdx.x; i < end; i += kThreads) c += results[i].x >= 0;
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+    if ((threadIdx.x & 63) == 0) waveSum[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int w = 0; w < kThreads / 64; w++) t += waveSum[w];
+        partial[blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void count_final_kernel(const int32_t* partial, int m, int32_t* out) {
+    __shared__ int waveSum[kThreads / 64];
+    int c = 0;
+    for (int i = (int)threadIdx.x; i < m; i += kThreads) c += partial[i];
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+    if ((threadIdx.x & 63) == 0) waveSum[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int w = 0; w < kThreads / 64; w++) t += waveSum[w];
+        *out = t;
+    }
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    return api_fail(MRT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+constexpr int kCountBlocks = 1024;
+
+}  // namespace
+}  // namespace mrt
+
+using namespace mrt;
+
+extern "C" {
+
+int mrt_raygen_primary(const float nscreenToWorld[16], const float origin[3], float maxDist, int32_t w, int32_t h,
+                       const int32_t* indexToPixel, void* rays, int32_t* slotToId, int32_t* idToSlot, void* stream) {
+    if (!nscreenToWorld || !origin || !indexToPixel || !rays) return api_fail(MRT_ERR_INVALID_ARG, "null argument");
+    if (w <= 0 || h <= 0 || (int64_t)w * h > INT32_MAX) return api_fail(MRT_ERR_INVALID_ARG, "bad image size");
+    PrimaryArgs a{};
+    for (int i = 0; i < 16; i++) a.m[i] = nscreenToWorld[i];
+    a.ox = origin[0]; a.oy = origin[1]; a.oz = origin[2];
+    a.maxDist = maxDist;
+    a.w = w; a.h = h;
+    a.indexToPixel = indexToPixel;
+    a.rays = static_cast<rg::RayRec*>(rays);
+    a.slotToId = slotToId;
+    a.idToSlot = idToSlot;
+    const int n = w * h;
+    hipLaunchKernelGGL(primary_kernel, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0,
+                       static_cast<hipStream_t>(stream), a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MRT_OK : hip_fail(e, "raygen primary launch");
+}
+
+int mrt_raygen_ao(const void* inRays, const void* inResults, int32_t numInputRays, const float* triNormals,
+                  int64_t numTris, int32_t numSamples, float maxDist, uint32_t seed, void* outRays,
+                  int32_t* outIdToSlot, int32_t* outSlotToId, void* stream) {
+    if (numInputRays < 0 || numSamples < 1) return api_fail(MRT_ERR_INVALID_ARG, "bad ray/sample count");
+    if (numInputRays == 0) return MRT_OK;
+    if (!inRays || !inResults || !outRays || (numTris > 0 && !triNormals))
+        return api_fail(MRT_ERR_INVALID_ARG, "null argument");
+    if ((int64_t)numInputRays * numSamples > INT32_MAX) return api_fail(MRT_ERR_TOO_LARGE, "too many output rays");
+    AOArgs a{};
+    a.inRays = static_cast<const rg::RayRec*>(inRays);
+    a.inResults = static_cast<const int2*>(inResults);
+    a.numInput = numInputRays;
+    a.normals = triNormals;
+    a.numTris = numTris;
+    a.numSamples = numSamples;
+    a.maxDist = maxDist;
+    a.seed = seed;
+    a.outRays = static_cast<rg::RayRec*>(outRays);
+    a.outIdToSlot = outIdToSlot;
+    a.outSlotToId = outSlotToId;
+    hipLaunchKernelGGL(ao_kernel, dim3((numInputRays + kThreads - 1) / kThreads), dim3(kThreads), 0,
+                       static_cast<hipStream_t>(stream), a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MRT_OK : hip_fail(e, "raygen ao launch");
+}
+
+int mrt_count_hits(const void* results, int32_t numRays, int32_t* hitCount, void* stream) {
+    if (!hitCount || numRays < 0 || (numRays > 0 && !results)) return api_fail(MRT_ERR_INVALID_ARG, "bad argument");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int perBlock = ((numRays + kCountBlocks - 1) / kCountBlocks + kThreads - 1) / kThreads * kThreads;
+    const int blocks = perBlock > 0 ? (numRays + perBlock - 1) / perBlock : 0;
+    // Stream-ordered scratch for the per-block partials (no state shared between calls).
+    int32_t* partial = nullptr;
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&partial), (size_t)(blocks + 1) * sizeof(int32_t), s);
+    if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(count partials)");
+    if (blocks > 0)
+        hipLaunchKernelGGL(count_partial_kernel, dim3(blocks), dim3(kThreads), 0, s,
+                           static_cast<const int4*>(results), numRays, perBlock, partial);
+    hipLaunchKernelGGL(count_final_kernel, dim3(1), dim3(kThreads), 0, s, partial, blocks, hitCount);
+    e = hipGetLastError();
+    const hipError_t f = hipFreeAsync(partial, s);
+    if (e != hipSuccess) return hip_fail(e, "count hits launch");
+    return f == hipSuccess ? MRT_OK : hip_fail(f, "hipFreeAsync(count partials)");
+}
+
+}  // extern "C"

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <string>
 
 namespace mrt {
 
@@ -61,5 +62,9 @@ hipError_t trace_occupancy(const TraceVariant& v, int* blocksPerCU);
 
 // Static facts about a variant's code object (for occupancy sizing/reporting).
 hipError_t trace_kernel_attributes(const TraceVariant& v, hipFuncAttributes* attr);
+
+// Thread-local error detail behind mrt_last_error_detail() (csrc/mrt_api.cpp).
+int api_fail(int code, const std::string& what);
+const char* api_last_error();
 
 }  // namespace mrt

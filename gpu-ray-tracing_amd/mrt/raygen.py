@@ -1,0 +1,80 @@
+"""Device ray generation and hit counting (mirror of the reference's RayGen,
+src/rt/ray/RayGen.cc:50-120, and countHitsKernel, RendererKernels.cu:112-162),
+over the mrt_raygen_* / mrt_count_hits entry points of include/mrt.h.
+
+The per-ray arithmetic is the host generator's (mrt.host.primary_rays /
+ao_rays): primary rays come out bit-identical, AO/diffuse directions within a
+few ulp (device cosf/sinf). Pixel tables and the camera matrix are computed on
+the host, as in the reference (PixelTable.cc, Renderer.cc:126-129).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib
+from .host import AO_SEED, Camera, Scene, pixel_table
+from .tracer import RayBuffer, _stream_ptr
+
+
+def nscreen_to_world(cam: Camera, w: int, h: int) -> np.ndarray:
+    out = (C.c_float * 16)()
+    c = cam.to_c()
+    _lib.check_host(_lib.host_lib().mrth_camera_nscreen_to_world(C.byref(c), w, h, out))
+    return np.array(out, np.float32)
+
+
+class DeviceRayGen:
+    """RayGen on one device: primary rays, AO/diffuse rays, hit counts."""
+
+    def __init__(self, scene: Scene | None = None, device=None):
+        self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.lib = _lib.trace_lib()
+        self._tables = {}
+        self.normals = None
+        self.num_tris = 0
+        if scene is not None:
+            _, _, normals = scene.arrays()
+            self.normals = torch.from_numpy(np.ascontiguousarray(normals, np.float32)).to(self.device)
+            self.num_tris = scene.num_triangles
+
+    def _table(self, w: int, h: int) -> torch.Tensor:
+        if (w, h) not in self._tables:
+            self._tables[(w, h)] = torch.from_numpy(pixel_table(w, h)).to(self.device)
+        return self._tables[(w, h)]
+
+    def primary(self, cam: Camera, w: int, h: int, stream=None) -> tuple[RayBuffer, torch.Tensor]:
+        """RayGen::primary: w*h closest-hit rays in Morton pixel order + slot->pixel ids."""
+        m = nscreen_to_world(cam, w, h)
+        origin = np.array(cam.position, np.float32)
+        rays = torch.empty((w * h, 8), dtype=torch.float32, device=self.device)
+        slot_to_id = torch.empty(w * h, dtype=torch.int32, device=self.device)
+        _lib.check(self.lib.mrt_raygen_primary(m.ctypes.data_as(C.POINTER(C.c_float)),
+                                               origin.ctypes.data_as(C.POINTER(C.c_float)), float(cam.far), w, h,
+                                               self._table(w, h).data_ptr(), rays.data_ptr(), slot_to_id.data_ptr(),
+                                               None, _stream_ptr(stream)))
+        return RayBuffer(rays, need_closest_hit=True, device=self.device), slot_to_id
+
+    def ao(self, rays: RayBuffer, num_samples: int, max_dist: float, seed: int = AO_SEED, closest_hit: bool = False,
+           stream=None) -> RayBuffer:
+        """RayGen::ao over a traced batch: num_samples hemisphere rays per input ray
+        (any-hit for AO; closest_hit=True with max_dist=far is the diffuse bounce)."""
+        if self.normals is None:
+            raise _lib.MrtError("DeviceRayGen.ao needs the scene's triangle normals (pass scene=)")
+        n = rays.size
+        out = torch.empty((n * num_samples, 8), dtype=torch.float32, device=self.device)
+        _lib.check(self.lib.mrt_raygen_ao(rays.rays.data_ptr(), rays.results.data_ptr(), n, self.normals.data_ptr(),
+                                          self.num_tris, num_samples, float(max_dist), seed & 0xFFFFFFFF,
+                                          out.data_ptr(), None, None, _stream_ptr(stream)))
+        return RayBuffer(out, need_closest_hit=closest_hit, device=self.device)
+
+    def count_hits_async(self, rays: RayBuffer, stream=None) -> torch.Tensor:
+        """Device int32 scalar: results with id >= 0 (no host sync)."""
+        out = torch.empty(1, dtype=torch.int32, device=self.device)
+        _lib.check(self.lib.mrt_count_hits(rays.results.data_ptr(), rays.size, out.data_ptr(), _stream_ptr(stream)))
+        return out
+
+    def count_hits(self, rays: RayBuffer, stream=None) -> int:
+        return int(self.count_hits_async(rays, stream).item())

@@ -112,6 +112,31 @@ int  mrt_tracer_trace(mrt_tracer* t, const void* rays, void* results, int32_t nu
 int  mrt_tracer_trace_timed(mrt_tracer* t, const void* rays, void* results, int32_t numRays,
                             uint32_t flags, int32_t* stats, void* stream, mrt_trace_info* info);
 
+/* ---- device ray generation and hit counting (the trace's producers and consumer) ----
+ * Stream-ordered on the calling thread's current HIP device. Buffers are device
+ * pointers; the camera matrix and origin are host values. Per-ray arithmetic is
+ * the host generator's (mrt_host.h mrth_primary_rays / mrth_ao_rays): primary
+ * rays are bit-identical to it (device denormals flush to zero), AO/diffuse
+ * directions agree to a few ulp (device cosf/sinf). */
+
+/* RayGen::primary + rayGenPrimaryKernel (RayGen.cc:50-72, RayGenKernels.cu:79-113).
+ * nscreenToWorld: column-major 4x4 (mrth_camera_nscreen_to_world). indexToPixel:
+ * w*h pixel ids in trace order (mrth_pixel_table). slotToId/idToSlot may be NULL. */
+int  mrt_raygen_primary(const float nscreenToWorld[16], const float origin[3], float maxDist, int32_t w, int32_t h,
+                        const int32_t* indexToPixel, void* rays, int32_t* slotToId, int32_t* idToSlot, void* stream);
+
+/* RayGen::ao + rayGenAOKernel (RayGen.cc:77-120, RayGenKernels.cu:117-227): numSamples
+ * hemisphere rays per input ray (origin backed off 1e-4 along the input ray, Halton
+ * (2,3) samples rotated by a Jenkins hash of seed + ray index, tmax = -1 for input
+ * misses). triNormals: 3 floats per triangle. Closest-hit use (diffuse): maxDist = far. */
+int  mrt_raygen_ao(const void* inRays, const void* inResults, int32_t numInputRays, const float* triNormals,
+                   int64_t numTris, int32_t numSamples, float maxDist, uint32_t seed, void* outRays,
+                   int32_t* outIdToSlot, int32_t* outSlotToId, void* stream);
+
+/* countHitsKernel (RendererKernels.cu:112-162): *hitCount (device int32) = number of
+ * results with id >= 0. */
+int  mrt_count_hits(const void* results, int32_t numRays, int32_t* hitCount, void* stream);
+
 /* ---- per-device convenience API (one implicit tracer per device) -------- */
 int  mrt_bind_bvh(const void* nodes, int64_t nodeBytes, const void* woop, int64_t woopBytes,
                   const int32_t* triIndex, int64_t triIndexBytes);

@@ -96,3 +96,32 @@ def test_empty_batch():
     nodes, woop, tri = kat.scene_two_floors()
     res, _, _ = O.trace(np.zeros((0, 8), np.float32), nodes, woop, tri)
     assert res.shape == (0, 4)
+
+
+def test_camera_matrix_export_reproduces_the_host_primary_rays():
+    """mrth_camera_nscreen_to_world (the matrix the device generator takes) with the
+    reference's per-ray formula (RayGenKernels.cu:88-110) gives the host rays."""
+    from mrt.raygen import nscreen_to_world
+    scene = mrt.Scene.synthetic("bunny", 0, 1)
+    cam, _ = scene.camera()
+    w, h = 48, 40
+    rays, slots = mrt.primary_rays(cam, w, h)
+    m = nscreen_to_world(cam, w, h).reshape(4, 4).T   # column-major -> [row][col]
+    f = np.float32
+    px = slots.astype(np.int64)
+    ns = np.stack([f(2) * ((px % w).astype(f) + f(0.5)) / f(w) - f(1), f(2) * ((px // w).astype(f) + f(0.5)) / f(h) - f(1),
+                   np.zeros(len(px), f), np.ones(len(px), f)], 1).astype(f)
+    wp4 = np.zeros((len(px), 4), f)
+    for i in range(4):
+        acc = np.zeros(len(px), f)
+        for j in range(4):
+            acc = (acc + m[i, j] * ns[:, j]).astype(f)
+        wp4[:, i] = acc
+    wp = wp4[:, :3] / wp4[:, 3:4]
+    d = (wp - np.array(cam.position, f)).astype(f)
+    dd = (f(0) + d[:, 0] * d[:, 0]).astype(f)
+    dd = (dd + d[:, 1] * d[:, 1]).astype(f)
+    dd = (dd + d[:, 2] * d[:, 2]).astype(f)
+    inv = (f(1) * (f(1) / np.sqrt(dd))).astype(f)
+    dirs = (d * inv[:, None]).astype(f)
+    assert np.array_equal(dirs.view(np.uint32), rays[:, 4:7].view(np.uint32))
