@@ -310,6 +310,20 @@ const char* mrt_error_string(int err) {
 
 const char* mrt_last_error_detail(void) { return mrt::api_last_error(); }
 
+int mrt_selftest_exact_rcp(uint64_t* mismatches) {
+    if (!mismatches) return fail(MRT_ERR_INVALID_ARG, "null argument");
+    unsigned long long* d = nullptr;
+    MRT_HIP(hipMalloc(&d, sizeof(*d)));
+    hipError_t e = hipMemset(d, 0, sizeof(*d));
+    if (e == hipSuccess) e = mrt::selftest_exact_rcp(d, nullptr);
+    unsigned long long h = 0;
+    if (e == hipSuccess) e = hipMemcpy(&h, d, sizeof(h), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return hipFail(e, "selftest_exact_rcp");
+    *mismatches = h;
+    return MRT_OK;
+}
+
 int mrt_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;

@@ -63,6 +63,10 @@ hipError_t trace_occupancy(const TraceVariant& v, int* blocksPerCU);
 // Static facts about a variant's code object (for occupancy sizing/reporting).
 hipError_t trace_kernel_attributes(const TraceVariant& v, hipFuncAttributes* attr);
 
+// Exhaustive check of the EXACT variants' reciprocal against 1.0f / x (all 2^32
+// inputs); adds the number of mismatching bit patterns to *mismatchesDev.
+hipError_t selftest_exact_rcp(unsigned long long* mismatchesDev, hipStream_t s);
+
 // Thread-local error detail behind mrt_last_error_detail() (csrc/mrt_api.cpp).
 int api_fail(int code, const std::string& what);
 const char* api_last_error();

@@ -71,6 +71,7 @@ TRACE_SYMBOLS = [
     ("mrt_raygen_primary", i32, [C.POINTER(f32), C.POINTER(f32), f32, i32, i32, vp, vp, vp, vp, vp]),
     ("mrt_raygen_ao", i32, [vp, vp, i32, vp, i64, i32, f32, u32, vp, vp, vp, vp]),
     ("mrt_count_hits", i32, [vp, i32, vp, vp]),
+    ("mrt_selftest_exact_rcp", i32, [C.POINTER(C.c_uint64)]),
     ("bind_CudaBVHTexture", None, [vp, i64, vp, i64, vp, i64]),
     ("unbind_CudaBVHTexture", None, []),
     ("launch_tracingKernel", f32, [i32, vp, C.c_int, C.c_bool, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),

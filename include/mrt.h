@@ -112,6 +112,11 @@ int  mrt_tracer_trace(mrt_tracer* t, const void* rays, void* results, int32_t nu
 int  mrt_tracer_trace_timed(mrt_tracer* t, const void* rays, void* results, int32_t numRays,
                             uint32_t flags, int32_t* stats, void* stream, mrt_trace_info* info);
 
+/* Diagnostics: run the EXACT variants' reciprocal (v_rcp_f32 + one FMA Newton step)
+ * against the correctly rounded 1.0f / x for all 2^32 inputs on the current device;
+ * *mismatches = number of differing bit patterns (0 expected). Blocking. */
+int  mrt_selftest_exact_rcp(uint64_t* mismatches);
+
 /* ---- device ray generation and hit counting (the trace's producers and consumer) ----
  * Stream-ordered on the calling thread's current HIP device. Buffers are device
  * pointers; the camera matrix and origin are host values. Per-ray arithmetic is

@@ -156,6 +156,15 @@ def test_fast_rcp_within_tolerance(tracer, wl):
     assert np.array_equal(res[~hit, 1], want[~hit, 1])   # misses keep tmax exactly
 
 
+def test_exact_reciprocal_is_correctly_rounded_for_every_float(tracer):
+    """The EXACT variants compute 1/x as v_rcp_f32 + one FMA Newton step; it must
+    equal the IEEE division 1.0f / x for all 2^32 inputs (device-side sweep)."""
+    from mrt import _lib
+    n = C.c_uint64(12345)
+    _lib.check(tracer.lib.mrt_selftest_exact_rcp(C.byref(n)))
+    assert n.value == 0
+
+
 # ---------------------------------------------------------------- launch configs
 @pytest.mark.parametrize("cfg", [dict(lds_stack=8), dict(lds_stack=32), dict(waves_per_cu=8),
                                  dict(num_queues=1), dict(num_queues=8, fetch_threshold=40),

@@ -34,6 +34,8 @@ def load(libdir):
         raise SystemExit(f"{path} is not linked -Bsymbolic; refusing to load it next to another copy")
     lib = C.CDLL(path, mode=C.RTLD_LOCAL)
     for name, res, args in _lib.TRACE_SYMBOLS:
+        if not hasattr(lib, name):   # an older build without a later entry point
+            continue
         fn = getattr(lib, name)
         fn.restype, fn.argtypes = res, args
     return lib
