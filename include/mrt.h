@@ -64,8 +64,9 @@ typedef struct mrt_launch_cfg {
     int32_t waves_per_cu;      /* persistent waves per CU (grid = CUs * waves_per_cu); 0 = auto (by batch size) */
     int32_t fetch_threshold;   /* refill a wave when fewer than this many of its 64 lanes are live (0 = when all are done)
                                   (reference DYNAMIC_FETCH_THRESHOLD 20 of 32, kepler_dynamic_fetch.cu:48) */
-    int32_t num_queues;        /* ray work queues (1..8, default 8 = one per XCD); -1 = static strided
-                                  assignment (lane L takes rays L, L+T, ...; no atomics)           */
+    int32_t num_queues;        /* -1 (default) = static strided rounds, no atomics; 1..8 = the reference's
+                                  dynamic fetch: a static first round, then one atomic per wave refill
+                                  on the queue of the wave's XCD (xcc % num_queues), no stealing      */
     int32_t lds_stack;         /* traversal-stack entries per lane kept in LDS: 8, 16 or 32       */
     int32_t node_levels;       /* binary BVH levels per node fetch: 1 = one Compact2 node; 2 = the node
                                   and both children's nodes in one 256-B treelet record (library-owned,
