@@ -306,7 +306,7 @@ def main():
     ap.add_argument("--fetch-threshold", type=int, default=-1)
     ap.add_argument("--lds-stack", type=int, default=0)
     ap.add_argument("--queues", type=int, default=0)
-    ap.add_argument("--node-levels", type=int, default=0)
+    ap.add_argument("--schedule", type=int, default=0, help="1 while-while, 2 if-if (0: library default)")
     ap.add_argument("--lane-groups", type=int, default=0)
     args = ap.parse_args()
 
@@ -324,8 +324,8 @@ def main():
         cfg["lds_stack"] = args.lds_stack
     if args.queues:
         cfg["num_queues"] = args.queues
-    if args.node_levels:
-        cfg["node_levels"] = args.node_levels
+    if args.schedule:
+        cfg["schedule"] = args.schedule
     if args.lane_groups:
         cfg["lane_groups"] = args.lane_groups
     if cfg:

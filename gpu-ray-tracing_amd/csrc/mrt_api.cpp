@@ -44,10 +44,6 @@ struct mrt_tracer {
     // round-trip that would otherwise sit on every launch).
     int occ[128] = {};
 
-    // Treelet records of the bound nodes (node_levels 2), built on first use.
-    void* treelets = nullptr;
-    size_t treeletCap = 0;
-    bool treeletsValid = false;
 };
 
 namespace mrt {
@@ -96,7 +92,7 @@ mrt_launch_cfg default_cfg() {
     c.fetch_threshold = 0;   // strided mode: a wave refills once all its lanes are done
     c.num_queues = -1;       // static strided assignment (see trace_kernel.hip); 1..8 = atomic queues
     c.lds_stack = 16;
-    c.node_levels = 1;
+    c.schedule = 1;
     c.lane_groups = 1;
     return c;
 }
@@ -104,7 +100,7 @@ mrt_launch_cfg default_cfg() {
 bool valid_cfg(const mrt_launch_cfg& c) {
     return (c.waves_per_cu == 0 || (c.waves_per_cu >= 4 && c.waves_per_cu <= 32)) && c.fetch_threshold >= 0 && c.fetch_threshold <= 64 &&
            (c.num_queues == -1 || (c.num_queues >= 1 && c.num_queues <= mrt::kMaxQueues)) &&
-           (c.lds_stack == 8 || c.lds_stack == 16 || c.lds_stack == 32) && (c.node_levels == 1 || c.node_levels == 2) &&
+           (c.lds_stack == 8 || c.lds_stack == 16 || c.lds_stack == 32) && (c.schedule == 1 || c.schedule == 2) &&
            c.lane_groups >= 1 && c.lane_groups <= 64 && (c.lane_groups & (c.lane_groups - 1)) == 0;
 }
 
@@ -115,8 +111,7 @@ mrt::TraceVariant variant_for(const mrt_tracer* t, uint32_t flags) {
     v.speculative = (flags & MRT_TRACE_LOCKSTEP_OFF) == 0;
     v.stats = (flags & MRT_TRACE_STATS) != 0;
     v.ldsStack = t->cfg.lds_stack;
-    // Treelet records are 4x the node buffer and addressed with 32-bit offsets.
-    v.treelet = t->cfg.node_levels == 2 && t->nodeBytes <= 0x3FFFFFF0ll;
+    v.ifif = t->cfg.schedule == 2;
     return v;
 }
 
@@ -137,7 +132,7 @@ constexpr int kAutoMinWaves = 8;
 int variant_key(const mrt::TraceVariant& v) {
     const int lds = v.ldsStack == 8 ? 0 : v.ldsStack == 16 ? 1 : 2;
     return (v.anyHit ? 1 : 0) | (v.speculative ? 2 : 0) | (v.exactRcp ? 4 : 0) | (v.stats ? 8 : 0) | (lds << 4) |
-           (v.treelet ? 64 : 0);
+           (v.ifif ? 64 : 0);
 }
 
 int grid_blocks(mrt_tracer* t, const mrt::TraceVariant& v, int numRays, int* outBlocksPerCU) {
@@ -224,21 +219,6 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     a.stats = reinterpret_cast<int4*>(stats);
 
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (v.treelet && !t->treeletsValid) {
-        const size_t bytes = (size_t)t->nodeBytes * 4;
-        if (bytes > t->treeletCap) {
-            if (t->treelets) MRT_HIP(hipFree(t->treelets));
-            t->treelets = nullptr;
-            t->treeletCap = 0;
-            MRT_HIP(hipMalloc(&t->treelets, bytes));
-            t->treeletCap = bytes;
-        }
-        MRT_HIP(mrt::build_treelets(t->nodes, (uint64_t)t->nodeBytes, t->treelets, s));
-        MRT_HIP(hipStreamSynchronize(s));   // once per bind: later traces may run on other streams
-        t->treeletsValid = true;
-    }
-    a.treelets = static_cast<const float4*>(t->treelets);
-    a.treeletBytes = v.treelet ? (uint32_t)(t->nodeBytes * 4) : 0u;
     // Queue heads restart at zero for every launch; strided mode has none.
     if (a.numQueues > 0)
         MRT_HIP(hipMemsetAsync(t->queues, 0, mrt::kMaxQueues * mrt::kQueueStrideWords * sizeof(unsigned), s));
@@ -251,7 +231,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
         info->grid_waves = totalLanes / 64;
         info->block_threads = mrt::kBlockThreads;
         info->lds_stack_entries = v.ldsStack;
-        info->node_levels = v.treelet ? 2 : 1;
+        info->schedule = v.ifif ? 2 : 1;
         int overflow = 0;
         MRT_HIP(hipMemcpy(&overflow, t->status, sizeof(int), hipMemcpyDeviceToHost));
         info->stack_overflows = overflow;
@@ -353,7 +333,6 @@ int mrt_tracer_destroy(mrt_tracer* t) {
         if (t->queues) (void)hipFree(t->queues);
         if (t->status) (void)hipFree(t->status);
         if (t->spill) (void)hipFree(t->spill);
-        if (t->treelets) (void)hipFree(t->treelets);
         if (t->evStart) (void)hipEventDestroy(t->evStart);
         if (t->evStop) (void)hipEventDestroy(t->evStop);
     }
@@ -367,7 +346,7 @@ int mrt_tracer_bind(mrt_tracer* t, const void* nodes, int64_t nodeBytes, const v
     if (nodeBytes < 64 || woopBytes < 16 || triIndexBytes < 4 || (nodeBytes % 64) || (woopBytes % 16) ||
         (triIndexBytes % 4))
         return fail(MRT_ERR_INVALID_ARG, "BVH buffer sizes are not Compact2-shaped");
-    if (nodeBytes > 0xFFFFFFF0ll || woopBytes > 0xFFFFFFF0ll)
+    if (nodeBytes > mrt::kMaxBufferBytes || woopBytes > mrt::kMaxBufferBytes)
         return fail(MRT_ERR_TOO_LARGE, "Compact2 buffer above the 32-bit buffer-offset range");
     if (triIndexBytes / 4 != woopBytes / 16) return fail(MRT_ERR_INVALID_ARG, "triIndex must hold one int per woop float4");
     std::lock_guard<std::mutex> lock(t->mu);
@@ -378,7 +357,6 @@ int mrt_tracer_bind(mrt_tracer* t, const void* nodes, int64_t nodeBytes, const v
     t->triIndex = triIndex;
     t->triIndexBytes = triIndexBytes;
     t->bound = true;
-    t->treeletsValid = false;   // rebuilt from the new nodes on the next node_levels-2 trace
     return MRT_OK;
 }
 
@@ -386,7 +364,6 @@ int mrt_tracer_unbind(mrt_tracer* t) {
     if (!t) return fail(MRT_ERR_INVALID_ARG, "null tracer");
     std::lock_guard<std::mutex> lock(t->mu);
     t->bound = false;
-    t->treeletsValid = false;
     t->nodes = t->woop = nullptr;
     t->triIndex = nullptr;
     return MRT_OK;
@@ -399,7 +376,7 @@ int mrt_tracer_set_config(mrt_tracer* t, const mrt_launch_cfg* cfg) {
     if (c.waves_per_cu == 0) c.waves_per_cu = d.waves_per_cu;
     if (c.num_queues == 0) c.num_queues = d.num_queues;
     if (c.lds_stack == 0) c.lds_stack = d.lds_stack;
-    if (c.node_levels == 0) c.node_levels = d.node_levels;
+    if (c.schedule == 0) c.schedule = d.schedule;
     if (c.lane_groups == 0) c.lane_groups = d.lane_groups;
     if (!valid_cfg(c)) return fail(MRT_ERR_INVALID_ARG, "launch config out of range");
     std::lock_guard<std::mutex> lock(t->mu);

@@ -18,18 +18,19 @@ constexpr int kStackCapacity = 64;
 constexpr int kMaxQueues = 8;
 constexpr int kQueueStrideWords = 64;      // one 256-B line per queue head
 constexpr int kBlockThreads = 256;         // 4 wave64s per workgroup
+// Largest node / woop buffer a tracer binds: offsets above it are out of range
+// for every buffer (the kernel's "no step" loads use 0xFFFFFFC0).
+constexpr int64_t kMaxBufferBytes = 0xFFFFFFC0ll;
 
 // Everything one launch needs; passed by value as the kernel argument.
 struct TraceArgs {
     const float4* rays;        // Ray[n] as 2 x float4
     int2* results;             // RayResult[n] viewed as int2 pairs; slot 2*i = {id, t}
     const float4* nodes;       // Compact2 nodes
-    const float4* treelets;    // treelet records (TREELET variants), 4 x nodeBytes
     const float4* woop;        // Woop triangles
     const int* triIndex;       // remap table
     uint32_t nodeBytes;        // buffer-resource ranges (range-checked loads)
     uint32_t woopBytes;
-    uint32_t treeletBytes;
     int numRays;
     int numQueues;             // 1..8 ray queues (per-XCD heads)
     int fetchThreshold;        // refill when fewer live lanes than this
@@ -48,11 +49,8 @@ struct TraceVariant {
     bool exactRcp;      // IEEE 1/x vs v_rcp_f32
     bool stats;
     int ldsStack;       // 8, 16 or 32 LDS entries per lane
-    bool treelet;       // fetch node + both children per round trip (treelet records)
+    bool ifif;          // if-if scheduling (one node or triangle step per lane per pass) vs while-while
 };
-
-// Treelet records for the bound BVH: records must hold 4 * nodeBytes bytes.
-hipError_t build_treelets(const void* nodes, uint64_t nodeBytes, void* records, hipStream_t s);
 
 // Launch one persistent trace. grid = number of 256-thread workgroups.
 hipError_t launch_trace(const TraceVariant& v, const TraceArgs& a, int gridBlocks, hipStream_t s);

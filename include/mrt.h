@@ -68,10 +68,11 @@ typedef struct mrt_launch_cfg {
                                   dynamic fetch: a static first round, then one atomic per wave refill
                                   on the queue of the wave's XCD (xcc % num_queues), no stealing      */
     int32_t lds_stack;         /* traversal-stack entries per lane kept in LDS: 8, 16 or 32       */
-    int32_t node_levels;       /* binary BVH levels per node fetch: 1 = one Compact2 node; 2 = the node
-                                  and both children's nodes in one 256-B treelet record (library-owned,
-                                  4 x nodeBytes, built from the bound nodes on first use; needs
-                                  nodeBytes < 1 GiB, else 1 is used). Same visit order and results. */
+    int32_t schedule;          /* 1 = while-while (the reference's: node loop until every lane holds a
+                                  leaf, then a leaf loop); 2 = if-if (each pass, every lane takes one
+                                  step — a node visit or one triangle slot — in its own order). Both
+                                  give the reference's results; if-if shortens the critical path of
+                                  divergent waves (profiles/round1_tuning.md). 0 = library default */
     int32_t lane_groups;       /* strided mode: a wave's 64 lanes take rays from this many (1..64, power of
                                   two) distant sub-ranges of the batch instead of 64 consecutive rays */
 } mrt_launch_cfg;
@@ -83,7 +84,7 @@ typedef struct mrt_trace_info {
     int32_t block_threads;     /* threads per workgroup                                           */
     int32_t lds_stack_entries; /* per-lane traversal-stack entries held in LDS                    */
     int32_t stack_overflows;   /* lanes that needed more than 64 stack entries (0 for SBVH depth<=64) */
-    int32_t node_levels;       /* binary levels per node fetch the launch used (1 or 2)           */
+    int32_t schedule;          /* traversal schedule the launch used (1 while-while, 2 if-if)     */
 } mrt_trace_info;
 
 /* ---- handle API -------------------------------------------------------- */

@@ -170,9 +170,10 @@ def test_exact_reciprocal_is_correctly_rounded_for_every_float(tracer):
                                  dict(num_queues=1), dict(num_queues=8, fetch_threshold=40),
                                  dict(num_queues=8, waves_per_cu=32, fetch_threshold=64),
                                  dict(num_queues=-1, fetch_threshold=16), dict(num_queues=-1, waves_per_cu=4),
-                                 dict(waves_per_cu=4, lds_stack=8, num_queues=3), dict(node_levels=1),
-                                 dict(node_levels=2, lds_stack=8, num_queues=3),
-                                 dict(node_levels=2, lds_stack=32, waves_per_cu=4), dict(lane_groups=2),
+                                 dict(waves_per_cu=4, lds_stack=8, num_queues=3), dict(schedule=1),
+                                 dict(schedule=2, lds_stack=8, num_queues=3),
+                                 dict(schedule=2, lds_stack=32, waves_per_cu=4, fetch_threshold=48),
+                                 dict(schedule=2, lane_groups=8), dict(lane_groups=2),
                                  dict(lane_groups=8), dict(lane_groups=64, waves_per_cu=4)],
                          ids=lambda c: ",".join(f"{k}={v}" for k, v in c.items()))
 def test_launch_configs_do_not_change_results(tracer, cfg):
@@ -189,32 +190,30 @@ def test_launch_configs_do_not_change_results(tracer, cfg):
 
 
 @pytest.mark.parametrize("wl", WORKLOADS, ids=lambda w: "-".join(map(str, w)))
-def test_treelet_fetch_is_bit_identical(tracer, wl):
-    """node_levels=2 (node + both children per round trip) visits the same nodes
-    in the same order: results and per-ray counters equal the oracle's."""
+def test_if_if_schedule_is_bit_identical(tracer, wl):
+    """schedule=2 (if-if) runs every lane in the reference's per-lane order: results
+    and per-ray counters equal the oracle's, closest and any hit alike."""
     bufs, rays, any_hit, want, st = scene_setup(*wl)
     saved = tracer.config()
-    for levels in (1, 2):
-        try:
-            tracer.set_config(node_levels=levels)
-            res, gst = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=False, stats=True)
-            assert tracer.last_info["node_levels"] == levels
+    try:
+        tracer.set_config(schedule=2)
+        for spec in (False, True):   # the speculation flag does not apply to if-if
+            res, gst = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=spec, stats=True)
+            assert tracer.last_info["schedule"] == 2
             assert np.array_equal(res[:, :2], want[:, :2]) and np.array_equal(gst[:, :3], st[:, :3])
-            res2, _ = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=True)
-            if any_hit:
-                assert_valid_hits(rays, res2, want, bufs)
-            else:
-                assert np.array_equal(res2[:, :2], want[:, :2])
-        finally:
-            tracer.set_config(**saved)
+    finally:
+        tracer.set_config(**saved)
 
 
-def test_treelets_follow_rebinding(tracer):
-    """The treelet records are rebuilt from whatever BVH is bound last."""
+def test_if_if_deep_stacks_and_rebinding(tracer):
+    """if-if with a 8-entry LDS ring (deep stacks spill) and a re-bound BVH."""
     saved = tracer.config()
     try:
-        tracer.set_config(node_levels=2)
+        tracer.set_config(schedule=2, lds_stack=8)
         test_rebinding_a_different_bvh(tracer)
+        bufs, rays, any_hit, want, st = scene_setup("sponza", 256, 192, "diffuse")
+        res, gst = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=False, stats=True)
+        assert np.array_equal(res[:, :2], want[:, :2]) and np.array_equal(gst[:, :3], st[:, :3])
     finally:
         tracer.set_config(**saved)
 
@@ -226,7 +225,7 @@ def test_invalid_config_rejected(tracer):
     with pytest.raises(MrtError):
         tracer.set_config(num_queues=9)
     with pytest.raises(MrtError):
-        tracer.set_config(node_levels=3)
+        tracer.set_config(schedule=3)
 
 
 # ---------------------------------------------------------------- edge cases

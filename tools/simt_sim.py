@@ -150,6 +150,63 @@ def simulate(nodes, woop, rays, K=1, frac=1.0, stream=False):
     return it_node, it_tri, passes, w.hit, w.hitT
 
 
+def simulate_ifif(nodes, woop, rays):
+    """'if-if' scheduling: every iteration each lane does one node visit or one
+    triangle slot; the wave pays a node pass and/or a triangle pass."""
+    w = Wave(nodes, woop, rays)
+    n = w.n
+    node = np.zeros(n, np.int64)
+    stack = [[SENT] for _ in range(n)]
+    leafpos = np.full(n, -1, np.int64)   # current woop slot when in a leaf
+    it_node = it_tri = 0
+
+    def inner(x):
+        return (x >= 0) & (x != SENT)
+    while True:
+        in_leaf = leafpos >= 0
+        act = np.nonzero(inner(node) & ~in_leaf)[0]
+        tri_l = np.nonzero(in_leaf)[0]
+        if len(act) == 0 and len(tri_l) == 0:
+            break
+        if len(act):
+            it_node += 1
+            t0, t1, swp, c0, c1 = w.boxes(act, node[act])
+            for j, L in enumerate(act):
+                if not t0[j] and not t1[j]:
+                    node[L] = stack[L].pop()
+                else:
+                    nx = c0[j] if t0[j] else c1[j]
+                    far = c1[j]
+                    if t0[j] and t1[j]:
+                        if swp[j]:
+                            nx, far = far, nx
+                        stack[L].append(far)
+                    node[L] = nx
+                if node[L] < 0:
+                    leafpos[L] = ~node[L]
+                    node[L] = stack[L].pop()
+        if len(tri_l):
+            it_tri += 1
+            for L in tri_l:
+                a = leafpos[L]
+                if w.wi[a, 0] == TERM:
+                    leafpos[L] = -1
+                else:
+                    # one triangle (reuse leaf_tris on a one-triangle view is awkward: inline)
+                    v0, v1, v2 = w.wf[a], w.wf[a + 1], w.wf[a + 2]
+                    o, d = w.o[L], w.d[L]
+                    Dz = d @ v0[:3]
+                    t = (v0[3] - o @ v0[:3]) / Dz if Dz != 0 else np.inf
+                    if w.tmin[L] < t < w.hitT[L]:
+                        u = (v1[3] + o @ v1[:3]) + t * (d @ v1[:3])
+                        v = (v2[3] + o @ v2[:3]) + t * (d @ v2[:3])
+                        if u >= 0 and v >= 0 and u + v <= 1:
+                            w.hitT[L] = t
+                            w.hit[L] = a
+                    leafpos[L] = a + 3
+    return it_node, it_tri
+
+
 def main():
     import bench
     import oracle_lib as O
@@ -179,6 +236,12 @@ def main():
             tot[i] += (a, b, c)
             line += f" {a:4d}/{b:4d}/{c:3d}"
         print(line, flush=True)
+    ifif = np.zeros(2)
+    for wi in pick:
+        a, b = simulate_ifif(nodes, woop, rays[wi * 64:(wi + 1) * 64])
+        ifif += (a, b)
+        print(f"  if-if wave {wi:6d}: node passes {a:4d} tri passes {b:4d}", flush=True)
+    print(f"  if-if total: node {ifif[0]:.0f} tri {ifif[1]:.0f}")
     for i, p in enumerate(policies):
         print(f"  {str(p):45s} node {tot[i][0]:8.0f} tri {tot[i][1]:8.0f} passes {tot[i][2]:6.0f} "
               f"sum {tot[i][0] + tot[i][1]:8.0f}")
