@@ -80,7 +80,9 @@ EXTRA_N1 = ["bunny-primary-640x480", "conference-ao-640x480", "sponza-diffuse-64
 # PMC-measured HBM traffic per launch (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in
 # separate passes, tools/profile_round.sh + tools/summarize_prof.py); counters
 # cannot be read inside this timed process, so the committed profile is cited.
-PMC_PROFILES = {"bunny-primary-1024x768": "profiles/round1_bunny1024_pmc_summary.json"}
+PMC_PROFILES = {w: f"profiles/round1_{w}_pmc_summary.json" for w in
+                ("bunny-primary-1024x768", "bunny-primary-640x480", "conference-ao-640x480", "sponza-diffuse-640x480",
+                 "hairball-diffuse-640x480")}
 
 
 def pmc_traffic(name):
@@ -98,18 +100,29 @@ def log(*a):
 
 
 # ----------------------------------------------------------------------------- setup
-def dist_setup(n_gpus):
+DIST_BACKEND = "nccl"
+
+
+def dist_setup(n_gpus, backend="nccl"):
+    """One process per GPU. backend "nccl" is RCCL; "gloo" (CPU collectives) is
+    only for rehearsing the N>1 flow with several ranks on one GPU."""
+    global DIST_BACKEND
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != n_gpus:
         raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
-    torch.cuda.set_device(local)
+    device = local if backend == "nccl" else local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    return rank, world, local
+        DIST_BACKEND = backend
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
+    return rank, world, device
 
 
 def barrier(world):
@@ -118,14 +131,22 @@ def barrier(world):
         dist.barrier()
 
 
-def bvh_for(scene_name, world, rank):
-    """Rank 0 builds the SBVH; the Compact2 buffers are broadcast over RCCL."""
-    import torch
+def bvh_for(scene_name, world, rank, cache_dir=None):
+    """Rank 0 builds the SBVH (or loads it from cache_dir/<scene>.dat, the
+    reference's bvhcache idea, Renderer.cc:157-217); the Compact2 buffers are
+    broadcast over RCCL."""
     import mrt
     scene = mrt.Scene.synthetic(scene_name, 0, 1)
     t0 = time.perf_counter()
     if rank == 0:
-        bvh = mrt.Bvh.build(scene)
+        path = os.path.join(cache_dir, f"{scene_name}.dat") if cache_dir else None
+        if path and os.path.exists(path):
+            bvh = mrt.Bvh.load(path)
+        else:
+            bvh = mrt.Bvh.build(scene)
+            if path:
+                os.makedirs(cache_dir, exist_ok=True)
+                bvh.save(path)
         bufs = bvh.buffers()
         stats = bvh.stats()
     else:
@@ -228,7 +249,7 @@ def max_over_ranks(x, world):
         return x
     import torch
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device="cuda" if DIST_BACKEND == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -253,9 +274,9 @@ def cpu_baseline(batches, bufs, threads):
             "parity_exact_fraction": exact}
 
 
-def run_workload(name, tracer, world, rank, steps, warmup, exact, want_cpu):
+def run_workload(name, tracer, world, rank, steps, warmup, exact, want_cpu, cache_dir=None):
     scene_name = workload_spec(name)[0]
-    scene, bufs, bstats, build_s = bvh_for(scene_name, world, rank)
+    scene, bufs, bstats, build_s = bvh_for(scene_name, world, rank, cache_dir)
     batches = Batches(name, scene, bufs, tracer)
     alg_bytes, n_nodes, n_tris, n_leaves = algorithmic_bytes(tracer, batches)
     wall, launch_ms = time_steps(tracer, batches, steps, warmup, world, exact)
@@ -307,13 +328,16 @@ def main():
     ap.add_argument("--lds-stack", type=int, default=0)
     ap.add_argument("--queues", type=int, default=0)
     ap.add_argument("--schedule", type=int, default=0, help="1 while-while, 2 if-if (0: library default)")
+    ap.add_argument("--bvh-cache", default=None, help="directory of <scene>.dat Compact2 caches (built if missing)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (RCCL) for real runs; gloo only to rehearse N>1 ranks on one GPU")
     ap.add_argument("--lane-groups", type=int, default=0)
     args = ap.parse_args()
 
     import torch
     from mrt.tracer import Tracer
 
-    rank, world, local = dist_setup(args.gpus)
+    rank, world, local = dist_setup(args.gpus, args.dist_backend)
     tracer = Tracer(local)
     cfg = {}
     if args.waves_per_cu:
@@ -333,13 +357,13 @@ def main():
     exact = args.rcp == "exact"
     want_cpu = (rank == 0 and world == 1 and not args.no_cpu)
 
-    head = run_workload(args.workload, tracer, world, rank, args.steps, args.warmup, exact, want_cpu)
+    head = run_workload(args.workload, tracer, world, rank, args.steps, args.warmup, exact, want_cpu, args.bvh_cache)
     extras = []
     do_extra = args.extra if args.extra is not None else (world == 1)
     if do_extra:
         for name in EXTRA_N1:
             if name != args.workload:
-                r = run_workload(name, tracer, world, rank, args.steps, args.warmup, exact, False)
+                r = run_workload(name, tracer, world, rank, args.steps, args.warmup, exact, False, args.bvh_cache)
                 extras.append(r)
                 log(f"[extra] {name}: {r['value']} Mrays/s (reference {r['reference_mrays']})")
 
