@@ -15,7 +15,10 @@ import os
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_DIR = os.environ.get("MRT_LIB_DIR") or os.path.join(PKG_DIR, "lib")
 TRACE_LIB_PATH = os.path.join(LIB_DIR, "libmrt.so")
-HOST_LIB_PATH = os.path.join(LIB_DIR, "libmrt_host.so")
+# A variant directory (tools/build_variant.sh) holds only libmrt.so; the host
+# library then comes from the regular build.
+HOST_LIB_PATH = os.path.join(LIB_DIR if os.path.exists(os.path.join(LIB_DIR, "libmrt_host.so"))
+                             else os.path.join(PKG_DIR, "lib"), "libmrt_host.so")
 
 # include/mrt.h
 MRT_TRACE_ANY_HIT = 1 << 0

@@ -60,3 +60,13 @@ def test_invalid_arguments_rejected_without_gpu():
         lib.mrt_tracer_destroy(out)
     assert lib.mrt_tracer_trace(None, None, None, 1, 0, None, None) == 1
     assert lib.mrt_tracer_bind(None, None, 0, None, 0, None, 0) == 1
+
+
+@pytest.mark.parametrize("struct,cls", [("mrt_launch_cfg", _lib.LaunchCfg), ("mrt_trace_info", _lib.TraceInfo)])
+def test_ctypes_structs_match_the_header(struct, cls):
+    """The Python mirrors of the C structs list the header's fields, in order."""
+    text = open(os.path.join(REPO, "include", "mrt.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    body = re.search(r"typedef struct " + struct + r"\s*\{(.*?)\}\s*" + struct + ";", text, flags=re.S).group(1)
+    fields = re.findall(r"\b(?:int32_t|float)\s+([A-Za-z_][A-Za-z0-9_]*)\s*;", body)
+    assert fields == [n for n, _ in cls._fields_]
