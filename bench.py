@@ -12,9 +12,15 @@ stand-ins with the published triangle counts (the OBJ assets are absent).
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME] [--extra/--no-extra]
 
 For N>1 launch with torch.distributed.run (one rank per GPU, RCCL): rank 0
-builds the SBVH and broadcasts the Compact2 buffers (the BVH is replicated);
-every rank traces its own full batch (weak scaling, no collective in the
-timed region); time = max over ranks. Rank 0 prints one JSON line.
+builds the SBVH and broadcasts the Compact2 buffers (the BVH is replicated).
+The job is N samples per pixel of the workload's view, sharded by sample:
+rank r traces the rays of sample r (rank 0's are the reference's pixel-centre
+rays; rank r > 0 samples each pixel at the r-th Halton (2,3) point), so every
+rank traces a distinct, equally sized and equally coherent batch (weak
+scaling, no collective in the timed region); time = max over ranks, value =
+rays counted on all ranks / time. After the timed steps the hit results are
+gathered to rank 0 over RCCL point-to-point (timed separately). Rank 0 prints
+one JSON line.
 """
 from __future__ import annotations
 
@@ -158,13 +164,28 @@ def bvh_for(scene_name, world, rank, cache_dir=None):
     return scene, bufs, stats, build_s
 
 
+def halton(i, base):
+    f, r = 1.0, 0.0
+    while i > 0:
+        f /= base
+        r += f * (i % base)
+        i //= base
+    return r
+
+
+def subpixel_sample(rank):
+    """Sample position inside the pixel for the shard of `rank`: the centre (the
+    reference's primary rays) for rank 0, the rank-th Halton (2,3) point otherwise."""
+    return (0.5, 0.5) if rank == 0 else (halton(rank, 2), halton(rank, 3))
+
+
 class Batches:
     """Ray batches of one workload, generated on the device like the reference
     Renderer (Renderer.cc:112-152,242-291; RayGen.cc:50-120): primary rays in
     Morton order; AO/diffuse rays from the traced primary hits (degenerate
     tmax=-1 rays for misses are traced too; only primary hits are counted)."""
 
-    def __init__(self, name, scene, bufs, tracer):
+    def __init__(self, name, scene, bufs, tracer, rank=0):
         from mrt.raygen import DeviceRayGen
         from mrt.tracer import GpuBvh
         sname, w, h, kind, bounces = workload_spec(name)
@@ -173,7 +194,7 @@ class Batches:
         tracer.set_bvh(self.gbvh)
         cam, ao_radius = scene.camera()
         gen = DeviceRayGen(scene)   # RayGen on the device (mrt_raygen_*), like the reference's RayGenKernels
-        prim, _ = gen.primary(cam, w, h)
+        prim, _ = gen.primary(cam, w, h, subpixel=subpixel_sample(rank))
         self.batches = []   # (RayBuffer, rays counted)
         if kind == "primary":
             self.batches.append((prim, w * h))
@@ -183,7 +204,7 @@ class Batches:
             for b in range(bounces):
                 hits = gen.count_hits(prev)
                 max_dist = ao_radius if kind == "ao" else cam.far
-                rb = gen.ao(prev, 1, max_dist, mrt_seed(b), closest_hit=(kind == "diffuse"))
+                rb = gen.ao(prev, 1, max_dist, mrt_seed(b) + 7919 * rank, closest_hit=(kind == "diffuse"))
                 self.batches.append((rb, hits))
                 if b + 1 < bounces:
                     tracer.trace_batch(rb, exact_rcp=True)
@@ -244,14 +265,38 @@ def time_steps(tracer, batches, steps, warmup, world, exact):
     return wall, launch_ms
 
 
-def max_over_ranks(x, world):
+def reduce_over_ranks(x, world, op="max"):
     if world == 1:
         return x
     import torch
     import torch.distributed as dist
     t = torch.tensor([x], dtype=torch.float64, device="cuda" if DIST_BACKEND == "nccl" else "cpu")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
     return float(t.item())
+
+
+def max_over_ranks(x, world):
+    return reduce_over_ranks(x, world, "max")
+
+
+def gather_to_root(batches, world):
+    """The hit-result gather that follows a sharded trace: every
+    rank's RayResult {id, t} of each batch to rank 0, RCCL point-to-point
+    (mrt/dist.py). Returns (ms, bytes received by rank 0)."""
+    import torch
+    from mrt.dist import gather_results
+    torch.cuda.synchronize()
+    barrier(world)
+    t0 = time.perf_counter()
+    nbytes = 0
+    for rb, _ in batches.batches:
+        res = rb.results if DIST_BACKEND == "nccl" else rb.results.cpu()
+        full = gather_results(res, world * rb.size)
+        if full is not None:
+            nbytes += full.numel() * 4
+    torch.cuda.synchronize()
+    ms = 1e3 * (time.perf_counter() - t0)
+    return max_over_ranks(ms, world), nbytes
 
 
 def cpu_baseline(batches, bufs, threads):
@@ -277,12 +322,17 @@ def cpu_baseline(batches, bufs, threads):
 def run_workload(name, tracer, world, rank, steps, warmup, exact, want_cpu, cache_dir=None):
     scene_name = workload_spec(name)[0]
     scene, bufs, bstats, build_s = bvh_for(scene_name, world, rank, cache_dir)
-    batches = Batches(name, scene, bufs, tracer)
+    batches = Batches(name, scene, bufs, tracer, rank)
     alg_bytes, n_nodes, n_tris, n_leaves = algorithmic_bytes(tracer, batches)
     wall, launch_ms = time_steps(tracer, batches, steps, warmup, world, exact)
     wall = max_over_ranks(wall, world)
+    launch_ms = max_over_ranks(launch_ms, world)
+    counted = int(reduce_over_ranks(batches.rays_counted, world, "sum"))
+    traced = int(reduce_over_ranks(batches.rays_traced, world, "sum"))
+    alg_bytes = reduce_over_ranks(alg_bytes, world, "sum") / world   # per-GPU launch bytes (mean over ranks)
     ms_per_step = 1e3 * wall / steps
-    value = world * batches.rays_counted * steps / wall / 1e6
+    value = counted * steps / wall / 1e6
+    gather = gather_to_root(batches, world) if world > 1 else None
     kernel_ms_per_step = launch_ms * len(batches.batches)
     achieved = alg_bytes / (kernel_ms_per_step * 1e-3) / 1e9
     out = {
@@ -292,7 +342,11 @@ def run_workload(name, tracer, world, rank, steps, warmup, exact, want_cpu, cach
         "kernel_ms_per_launch": round(launch_ms, 4),
         "rays_counted": batches.rays_counted,
         "rays_traced": batches.rays_traced,
-        "mrays_traced_per_s": round(world * batches.rays_traced * steps / wall / 1e6, 2),
+        "mrays_traced_per_s": round(traced * steps / wall / 1e6, 2),
+        "rays_counted_all_ranks": counted,
+        "gather": ({"ms": round(gather[0], 3), "bytes_to_root": gather[1],
+                    "value_incl_gather": round(counted * steps / (wall + steps * gather[0] / 1e3) / 1e6, 2)}
+                   if gather else None),
         "scene_tris": scene.num_triangles,
         "bvh": {"inner_nodes": len(bufs[0]) // 16, "woop_slots": len(bufs[1]) // 4,
                 "bytes": 4 * (len(bufs[0]) + len(bufs[1]) + len(bufs[2])), "build_s": round(build_s, 2),
@@ -386,12 +440,14 @@ def main():
                        "scene_tris": head["scene_tris"], "width": workload_spec(args.workload)[1],
                        "height": workload_spec(args.workload)[2], "ray_type": workload_spec(args.workload)[3],
                        "rays_per_gpu": head["rays_counted"], "rcp": args.rcp,
-                       "parallelism": f"rays replicated-BVH x{world} (weak, no collective in step)",
+                       "parallelism": (f"rays sharded by pixel sample x{world}, BVH replicated "
+                                       f"(weak: one {workload_spec(args.workload)[1]}x{workload_spec(args.workload)[2]} "
+                                       f"sample per GPU, no collective in the step)"),
                        "tracer": tracer.config()},
             "roofline": head["roofline"],
             "cpu_baseline": head.get("cpu_baseline"),
             "detail": {k: head[k] for k in ("kernel_ms_per_launch", "rays_traced", "mrays_traced_per_s", "bvh",
-                                            "per_ray", "reference_mrays")},
+                                            "per_ray", "reference_mrays", "rays_counted_all_ranks", "gather")},
             "extra_workloads": [{k: r[k] for k in ("workload", "value", "reference_mrays", "kernel_ms_per_launch",
                                                    "rays_counted", "rays_traced", "per_ray", "roofline", "bvh")}
                                 for r in extras],

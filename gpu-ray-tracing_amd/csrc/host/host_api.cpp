@@ -221,6 +221,14 @@ int mrth_primary_rays(const mrth_camera* cam, int32_t w, int32_t h, void* rays, 
     return MRTH_OK;
 }
 
+int mrth_primary_rays_subpixel(const mrth_camera* cam, int32_t w, int32_t h, float jx, float jy, void* rays,
+                               int32_t* slotToId) {
+    if (!cam || w <= 0 || h <= 0 || !rays) return fail(MRTH_ERR_INVALID_ARG, "bad arguments");
+    if (!(jx >= 0.0f && jx < 1.0f && jy >= 0.0f && jy < 1.0f)) return fail(MRTH_ERR_INVALID_ARG, "subpixel offset outside [0, 1)");
+    mrt::gen_primary_rays(to_camera(cam), w, h, static_cast<mrt::Ray*>(rays), slotToId, jx, jy);
+    return MRTH_OK;
+}
+
 int mrth_camera_nscreen_to_world(const mrth_camera* cam, int32_t w, int32_t h, float out[16]) {
     if (!cam || w <= 0 || h <= 0 || !out) return fail(MRTH_ERR_INVALID_ARG, "bad arguments");
     const mrt::Mat4f m = mrt::nscreen_to_world(to_camera(cam), w, h);

@@ -116,14 +116,14 @@ std::vector<int32_t> pixel_table(int w, int h) {   // PixelTable.cc:70-161 ("sma
     return idxToPos;
 }
 
-void gen_primary_rays(const Camera& cam, int w, int h, Ray* out, int32_t* slotToId) {
+void gen_primary_rays(const Camera& cam, int w, int h, Ray* out, int32_t* slotToId, float jx, float jy) {
     const Mat4f m = nscreen_to_world(cam, w, h);
     const std::vector<int32_t> table = pixel_table(w, h);
     const rg::V3 origin = rg::make(cam.position.x, cam.position.y, cam.position.z);
     parallel_for((int64_t)w * h, [&](int64_t lo, int64_t hi) {
         for (int64_t task = lo; task < hi; task++) {
             const int pixel = table[task];
-            const rg::RayRec r = rg::primary_ray(m.m, origin, cam.farDist, w, h, pixel);
+            const rg::RayRec r = rg::primary_ray(m.m, origin, cam.farDist, w, h, pixel, jx, jy);
             std::memcpy(&out[task], &r, sizeof(Ray));
             if (slotToId) slotToId[task] = pixel;
         }

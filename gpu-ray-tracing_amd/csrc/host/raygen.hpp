@@ -25,7 +25,7 @@ static_assert(sizeof(RayResult) == 16, "RayResult must be 16 bytes");
 
 Mat4f nscreen_to_world(const Camera& cam, int w, int h);
 std::vector<int32_t> pixel_table(int w, int h);
-void gen_primary_rays(const Camera& cam, int w, int h, Ray* out, int32_t* slotToId);
+void gen_primary_rays(const Camera& cam, int w, int h, Ray* out, int32_t* slotToId, float jx = 0.5f, float jy = 0.5f);
 void gen_ao_rays(const Ray* inRays, const RayResult* inResults, int64_t numInput, const Vec3f* triNormals,
                  int64_t numTris, int numSamples, float maxDist, uint32_t seed, Ray* out);
 int64_t count_hits(const RayResult* results, int64_t n);

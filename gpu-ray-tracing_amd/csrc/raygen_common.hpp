@@ -69,10 +69,12 @@ MRT_HD inline float rg_sin(float x) {
 
 constexpr float kPi = 3.14159265358979323846f;
 
-// m: column-major 4x4 nscreen-to-world matrix, (r, c) at m[c * 4 + r].
-MRT_HD inline RayRec primary_ray(const float* m, V3 origin, float maxDist, int w, int h, int pixel) {
-    const float ns[4] = {2.0f * ((float)(pixel % w) + 0.5f) / (float)w - 1.0f,
-                         2.0f * ((float)(pixel / w) + 0.5f) / (float)h - 1.0f, 0.0f, 1.0f};
+// m: column-major 4x4 nscreen-to-world matrix, (r, c) at m[c * 4 + r]. (jx, jy):
+// position inside the pixel; the reference always uses the centre (0.5, 0.5).
+MRT_HD inline RayRec primary_ray(const float* m, V3 origin, float maxDist, int w, int h, int pixel, float jx = 0.5f,
+                                 float jy = 0.5f) {
+    const float ns[4] = {2.0f * ((float)(pixel % w) + jx) / (float)w - 1.0f,
+                         2.0f * ((float)(pixel / w) + jy) / (float)h - 1.0f, 0.0f, 1.0f};
     float wp4[4];
     for (int i = 0; i < 4; i++) {
         float rr = 0.0f;

@@ -28,6 +28,7 @@ constexpr int kThreads = 256;
 struct PrimaryArgs {
     float m[16];   // column-major nscreen-to-world
     float ox, oy, oz, maxDist;
+    float jx, jy;   // sample position inside the pixel
     int w, h;
     const int32_t* indexToPixel;
     rg::RayRec* rays;
@@ -39,7 +40,7 @@ __global__ __launch_bounds__(kThreads) void primary_kernel(PrimaryArgs a) {
     const int task = (int)(blockIdx.x * kThreads + threadIdx.x);
     if (task >= a.w * a.h) return;
     const int pixel = a.indexToPixel[task];
-    a.rays[task] = rg::primary_ray(a.m, rg::make(a.ox, a.oy, a.oz), a.maxDist, a.w, a.h, pixel);
+    a.rays[task] = rg::primary_ray(a.m, rg::make(a.ox, a.oy, a.oz), a.maxDist, a.w, a.h, pixel, a.jx, a.jy);
     if (a.slotToId) a.slotToId[task] = pixel;
     if (a.idToSlot) a.idToSlot[pixel] = task;
 }
@@ -119,9 +120,19 @@ extern "C" {
 
 int mrt_raygen_primary(const float nscreenToWorld[16], const float origin[3], float maxDist, int32_t w, int32_t h,
                        const int32_t* indexToPixel, void* rays, int32_t* slotToId, int32_t* idToSlot, void* stream) {
+    return mrt_raygen_primary_subpixel(nscreenToWorld, origin, maxDist, w, h, 0.5f, 0.5f, indexToPixel, rays, slotToId,
+                                       idToSlot, stream);
+}
+
+int mrt_raygen_primary_subpixel(const float nscreenToWorld[16], const float origin[3], float maxDist, int32_t w,
+                                int32_t h, float jx, float jy, const int32_t* indexToPixel, void* rays,
+                                int32_t* slotToId, int32_t* idToSlot, void* stream) {
     if (!nscreenToWorld || !origin || !indexToPixel || !rays) return api_fail(MRT_ERR_INVALID_ARG, "null argument");
     if (w <= 0 || h <= 0 || (int64_t)w * h > INT32_MAX) return api_fail(MRT_ERR_INVALID_ARG, "bad image size");
+    if (!(jx >= 0.0f && jx < 1.0f && jy >= 0.0f && jy < 1.0f)) return api_fail(MRT_ERR_INVALID_ARG, "subpixel offset outside [0, 1)");
     PrimaryArgs a{};
+    a.jx = jx;
+    a.jy = jy;
     for (int i = 0; i < 16; i++) a.m[i] = nscreenToWorld[i];
     a.ox = origin[0]; a.oy = origin[1]; a.oz = origin[2];
     a.maxDist = maxDist;

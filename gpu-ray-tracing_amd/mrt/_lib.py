@@ -72,6 +72,8 @@ TRACE_SYMBOLS = [
     ("mrt_version", i32, []),
     ("mrt_device_count", i32, []),
     ("mrt_raygen_primary", i32, [C.POINTER(f32), C.POINTER(f32), f32, i32, i32, vp, vp, vp, vp, vp]),
+    ("mrt_raygen_primary_subpixel", i32, [C.POINTER(f32), C.POINTER(f32), f32, i32, i32, f32, f32, vp, vp, vp, vp,
+                                          vp]),
     ("mrt_raygen_ao", i32, [vp, vp, i32, vp, i64, i32, f32, u32, vp, vp, vp, vp]),
     ("mrt_count_hits", i32, [vp, i32, vp, vp]),
     ("mrt_selftest_exact_rcp", i32, [C.POINTER(C.c_uint64)]),
@@ -103,6 +105,7 @@ HOST_SYMBOLS = [
     ("mrth_woopify", None, [C.POINTER(f32), C.POINTER(f32), C.POINTER(f32), C.POINTER(f32)]),
     ("mrth_pixel_table", i32, [i32, i32, vp]),
     ("mrth_primary_rays", i32, [C.POINTER(HostCamera), i32, i32, vp, vp]),
+    ("mrth_primary_rays_subpixel", i32, [C.POINTER(HostCamera), i32, i32, f32, f32, vp, vp]),
     ("mrth_camera_nscreen_to_world", i32, [C.POINTER(HostCamera), i32, i32, C.POINTER(f32)]),
     ("mrth_ao_rays", i32, [vp, vp, i64, vp, i32, f32, u32, vp]),
     ("mrth_count_hits", i64, [vp, i64]),

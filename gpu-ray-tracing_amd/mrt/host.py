@@ -177,11 +177,17 @@ def pixel_table(w: int, h: int) -> np.ndarray:
     return out
 
 
-def primary_rays(cam: Camera, w: int, h: int):
+def primary_rays(cam: Camera, w: int, h: int, subpixel=(0.5, 0.5)):
+    """RayGen::primary (RayGen.cc:50-72): w*h rays in Morton pixel order + slot->pixel ids.
+    subpixel: sample position inside each pixel (the reference's is the centre)."""
     rays = np.empty((w * h, 8), np.float32)
     slot_to_id = np.empty(w * h, np.int32)
     c = cam.to_c()
-    _lib.check_host(_lib.host_lib().mrth_primary_rays(C.byref(c), w, h, _ptr(rays), _ptr(slot_to_id)))
+    if tuple(subpixel) == (0.5, 0.5):
+        _lib.check_host(_lib.host_lib().mrth_primary_rays(C.byref(c), w, h, _ptr(rays), _ptr(slot_to_id)))
+    else:
+        _lib.check_host(_lib.host_lib().mrth_primary_rays_subpixel(C.byref(c), w, h, float(subpixel[0]),
+                                                                   float(subpixel[1]), _ptr(rays), _ptr(slot_to_id)))
     return rays, slot_to_id
 
 

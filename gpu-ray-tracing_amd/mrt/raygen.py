@@ -45,16 +45,18 @@ class DeviceRayGen:
             self._tables[(w, h)] = torch.from_numpy(pixel_table(w, h)).to(self.device)
         return self._tables[(w, h)]
 
-    def primary(self, cam: Camera, w: int, h: int, stream=None) -> tuple[RayBuffer, torch.Tensor]:
-        """RayGen::primary: w*h closest-hit rays in Morton pixel order + slot->pixel ids."""
+    def primary(self, cam: Camera, w: int, h: int, stream=None, subpixel=(0.5, 0.5)) -> tuple[RayBuffer, torch.Tensor]:
+        """RayGen::primary: w*h closest-hit rays in Morton pixel order + slot->pixel ids.
+        subpixel: sample position inside each pixel (the reference's is the centre)."""
         m = nscreen_to_world(cam, w, h)
         origin = np.array(cam.position, np.float32)
         rays = torch.empty((w * h, 8), dtype=torch.float32, device=self.device)
         slot_to_id = torch.empty(w * h, dtype=torch.int32, device=self.device)
-        _lib.check(self.lib.mrt_raygen_primary(m.ctypes.data_as(C.POINTER(C.c_float)),
-                                               origin.ctypes.data_as(C.POINTER(C.c_float)), float(cam.far), w, h,
-                                               self._table(w, h).data_ptr(), rays.data_ptr(), slot_to_id.data_ptr(),
-                                               None, _stream_ptr(stream)))
+        _lib.check(self.lib.mrt_raygen_primary_subpixel(m.ctypes.data_as(C.POINTER(C.c_float)),
+                                                        origin.ctypes.data_as(C.POINTER(C.c_float)), float(cam.far), w,
+                                                        h, float(subpixel[0]), float(subpixel[1]),
+                                                        self._table(w, h).data_ptr(), rays.data_ptr(),
+                                                        slot_to_id.data_ptr(), None, _stream_ptr(stream)))
         return RayBuffer(rays, need_closest_hit=True, device=self.device), slot_to_id
 
     def ao(self, rays: RayBuffer, num_samples: int, max_dist: float, seed: int = AO_SEED, closest_hit: bool = False,

@@ -132,6 +132,13 @@ int  mrt_selftest_exact_rcp(uint64_t* mismatches);
 int  mrt_raygen_primary(const float nscreenToWorld[16], const float origin[3], float maxDist, int32_t w, int32_t h,
                         const int32_t* indexToPixel, void* rays, int32_t* slotToId, int32_t* idToSlot, void* stream);
 
+/* The same rays sampled at (jx, jy) in [0, 1)^2 inside each pixel instead of its centre
+ * (0.5, 0.5): distinct, equally coherent batches of one view, e.g. one sample per rank
+ * when a frame's rays are sharded over GPUs (bench.py). */
+int  mrt_raygen_primary_subpixel(const float nscreenToWorld[16], const float origin[3], float maxDist, int32_t w,
+                                 int32_t h, float jx, float jy, const int32_t* indexToPixel, void* rays,
+                                 int32_t* slotToId, int32_t* idToSlot, void* stream);
+
 /* RayGen::ao + rayGenAOKernel (RayGen.cc:77-120, RayGenKernels.cu:117-227): numSamples
  * hemisphere rays per input ray (origin backed off 1e-4 along the input ray, Halton
  * (2,3) samples rotated by a Jenkins hash of seed + ray index, tmax = -1 for input

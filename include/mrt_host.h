@@ -82,6 +82,9 @@ void mrth_woopify(const float v0[3], const float v1[3], const float v2[3], float
 int  mrth_pixel_table(int32_t w, int32_t h, int32_t* indexToPixel /* w*h */);
 int  mrth_primary_rays(const mrth_camera* cam, int32_t w, int32_t h, void* rays /* w*h Ray */,
                        int32_t* slotToId /* w*h or NULL */);
+/* Primary rays sampled at (jx, jy) in [0, 1)^2 inside each pixel (centre = 0.5, 0.5). */
+int  mrth_primary_rays_subpixel(const mrth_camera* cam, int32_t w, int32_t h, float jx, float jy, void* rays,
+                                int32_t* slotToId);
 /* invert(fitToView(-1, 2, (w, h)) * worldToClip), column-major (Renderer.cc:126-129): the
  * matrix mrt_raygen_primary (mrt.h) takes. */
 int  mrth_camera_nscreen_to_world(const mrth_camera* cam, int32_t w, int32_t h, float out[16]);

@@ -26,6 +26,15 @@ def ftz(a):
     return a
 
 
+@pytest.mark.parametrize("subpixel", [(0.25, 0.75), (0.0, 0.999)])
+def test_subpixel_primary_rays_match_the_host_bit_for_bit(gen, subpixel):
+    scene = mrt.Scene.synthetic("bunny", 0, 1)
+    cam, _ = scene.camera()
+    host_rays, _ = mrt.primary_rays(cam, 160, 120, subpixel=subpixel)
+    rb, _ = gen(scene).primary(cam, 160, 120, subpixel=subpixel)
+    assert np.array_equal(rb.rays.cpu().numpy().view(np.uint32), ftz(host_rays).view(np.uint32))
+
+
 @pytest.mark.parametrize("scene_name,w,h", [("bunny", 320, 240), ("conference", 333, 217), ("mori", 64, 9),
                                             ("sponza", 1, 1)])
 def test_primary_rays_match_the_host_bit_for_bit(gen, scene_name, w, h):

@@ -98,18 +98,20 @@ def test_empty_batch():
     assert res.shape == (0, 4)
 
 
-def test_camera_matrix_export_reproduces_the_host_primary_rays():
+@pytest.mark.parametrize("jx,jy", [(0.5, 0.5), (0.25, 0.875)])
+def test_camera_matrix_export_reproduces_the_host_primary_rays(jx, jy):
     """mrth_camera_nscreen_to_world (the matrix the device generator takes) with the
-    reference's per-ray formula (RayGenKernels.cu:88-110) gives the host rays."""
+    reference's per-ray formula (RayGenKernels.cu:88-110) gives the host rays, at the
+    pixel centre (the reference) and at another sample position inside the pixel."""
     from mrt.raygen import nscreen_to_world
     scene = mrt.Scene.synthetic("bunny", 0, 1)
     cam, _ = scene.camera()
     w, h = 48, 40
-    rays, slots = mrt.primary_rays(cam, w, h)
+    rays, slots = mrt.primary_rays(cam, w, h, subpixel=(jx, jy))
     m = nscreen_to_world(cam, w, h).reshape(4, 4).T   # column-major -> [row][col]
     f = np.float32
     px = slots.astype(np.int64)
-    ns = np.stack([f(2) * ((px % w).astype(f) + f(0.5)) / f(w) - f(1), f(2) * ((px // w).astype(f) + f(0.5)) / f(h) - f(1),
+    ns = np.stack([f(2) * ((px % w).astype(f) + f(jx)) / f(w) - f(1), f(2) * ((px // w).astype(f) + f(jy)) / f(h) - f(1),
                    np.zeros(len(px), f), np.ones(len(px), f)], 1).astype(f)
     wp4 = np.zeros((len(px), 4), f)
     for i in range(4):
