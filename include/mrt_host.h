@@ -52,7 +52,7 @@ typedef struct mrth_bvh_stats {
 
 /* ---- scenes -------------------------------------------------------------- */
 /* name: "mori" | "bunny" | "conference" | "sponza" | "hairball" (published
- * triangle counts), "sphere" (param = rings), "random" (param = triangles). */
+ * triangle counts; "hairball" with param > 0: that many tubes, unpadded), "sphere" (param = rings), "random" (param = triangles). */
 int  mrth_scene_synthetic(const char* name, int64_t param, uint64_t seed, mrth_scene** out);
 int  mrth_scene_load_obj(const char* path, mrth_scene** out);
 int  mrth_scene_from_arrays(const float* vertices, int64_t numVertices, const int32_t* triangles,

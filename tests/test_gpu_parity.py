@@ -107,7 +107,8 @@ SCENE_CACHE = {}
 def scene_setup(name, w, h, kind):
     key = (name, w, h, kind)
     if key not in SCENE_CACHE:
-        scene = mrt.Scene.synthetic(name, 0, 1)
+        base, _, param = name.partition(":")   # "hairball:800" = an 800-tube hairball
+        scene = mrt.Scene.synthetic(base, int(param or 0), 1)
         bufs = mrt.Bvh.build(scene).buffers()
         cam, ao = scene.camera()
         rays, _ = mrt.primary_rays(cam, w, h)
@@ -121,7 +122,7 @@ def scene_setup(name, w, h, kind):
 
 
 WORKLOADS = [("bunny", 320, 240, "primary"), ("conference", 256, 192, "ao"), ("sponza", 256, 192, "diffuse"),
-             ("conference", 256, 192, "diffuse"), ("mori", 256, 192, "ao")]
+             ("conference", 256, 192, "diffuse"), ("mori", 256, 192, "ao"), ("hairball:800", 256, 192, "diffuse")]
 
 
 @pytest.mark.parametrize("wl", WORKLOADS, ids=lambda w: "-".join(map(str, w)))
