@@ -38,11 +38,14 @@ struct mrt_tracer {
     int* status = nullptr;        // overflow counter
     int* spill = nullptr;
     size_t spillInts = 0;
+    unsigned* tailCount = nullptr;   // two record counters, used by alternate exporting launches
+    int* tailRec = nullptr;          // kTailWords x kTailCapacity words
+    unsigned tailEpoch = 0;          // exporting launches so far
     hipEvent_t evStart = nullptr, evStop = nullptr;
 
     // Occupancy per kernel variant, queried once (hipOccupancy* is a host
     // round-trip that would otherwise sit on every launch).
-    int occ[128] = {};
+    int occ[256] = {};
 
 };
 
@@ -86,6 +89,13 @@ struct DeviceGuard {
     }
 };
 
+// Tail export / resume defaults (profiles/round1_tuning.md, "Tail export").
+constexpr int kDefaultTailLanes = -1;
+constexpr int kDefaultTailAfterUs = 30;
+constexpr int kDefaultTailResumeLanes = 1;
+constexpr int kDefaultTailResumeWaves = 28;   // capped by the resume kernel's occupancy
+constexpr int kTailCapacity = 1 << 16;   // records (22 MB)
+
 mrt_launch_cfg default_cfg() {
     mrt_launch_cfg c;
     c.waves_per_cu = 0;   // auto: sized from the batch (grid_blocks)
@@ -94,6 +104,10 @@ mrt_launch_cfg default_cfg() {
     c.lds_stack = 16;
     c.schedule = 1;
     c.lane_groups = 1;
+    c.tail_lanes = kDefaultTailLanes;
+    c.tail_after_us = kDefaultTailAfterUs;
+    c.tail_resume_lanes = kDefaultTailResumeLanes;
+    c.tail_resume_waves = kDefaultTailResumeWaves;
     return c;
 }
 
@@ -101,7 +115,10 @@ bool valid_cfg(const mrt_launch_cfg& c) {
     return (c.waves_per_cu == 0 || (c.waves_per_cu >= 4 && c.waves_per_cu <= 32)) && c.fetch_threshold >= 0 && c.fetch_threshold <= 64 &&
            (c.num_queues == -1 || (c.num_queues >= 1 && c.num_queues <= mrt::kMaxQueues)) &&
            (c.lds_stack == 8 || c.lds_stack == 16 || c.lds_stack == 32) && (c.schedule == 1 || c.schedule == 2) &&
-           c.lane_groups >= 1 && c.lane_groups <= 64 && (c.lane_groups & (c.lane_groups - 1)) == 0;
+           c.lane_groups >= 1 && c.lane_groups <= 64 && (c.lane_groups & (c.lane_groups - 1)) == 0 &&
+           (c.tail_lanes == -1 || (c.tail_lanes >= 1 && c.tail_lanes <= 64)) && c.tail_after_us >= 1 &&
+           c.tail_after_us <= 100000 && c.tail_resume_lanes >= 1 && c.tail_resume_lanes <= 64 &&
+           c.tail_resume_waves >= 4 && c.tail_resume_waves <= 32 && c.tail_resume_waves % 4 == 0;
 }
 
 mrt::TraceVariant variant_for(const mrt_tracer* t, uint32_t flags) {
@@ -132,7 +149,7 @@ constexpr int kAutoMinWaves = 8;
 int variant_key(const mrt::TraceVariant& v) {
     const int lds = v.ldsStack == 8 ? 0 : v.ldsStack == 16 ? 1 : 2;
     return (v.anyHit ? 1 : 0) | (v.speculative ? 2 : 0) | (v.exactRcp ? 4 : 0) | (v.stats ? 8 : 0) | (lds << 4) |
-           (v.ifif ? 64 : 0);
+           (v.ifif ? 64 : 0) | (v.resume ? 128 : 0);
 }
 
 int grid_blocks(mrt_tracer* t, const mrt::TraceVariant& v, int numRays, int* outBlocksPerCU) {
@@ -160,7 +177,7 @@ int grid_blocks(mrt_tracer* t, const mrt::TraceVariant& v, int numRays, int* out
     return perCU * t->numCUs;
 }
 
-int ensure_workspace(mrt_tracer* t, int totalLanes, int ldsStack) {
+int ensure_workspace(mrt_tracer* t, int totalLanes, int ldsStack, bool tail) {
     if (!t->queues) {
         MRT_HIP(hipMalloc(&t->queues, mrt::kMaxQueues * mrt::kQueueStrideWords * sizeof(unsigned)));
         MRT_HIP(hipMalloc(&t->status, 64 * sizeof(int)));
@@ -173,6 +190,11 @@ int ensure_workspace(mrt_tracer* t, int totalLanes, int ldsStack) {
         t->spillInts = 0;
         MRT_HIP(hipMalloc(&t->spill, need * sizeof(int)));
         t->spillInts = need;
+    }
+    if (tail && !t->tailCount) {
+        MRT_HIP(hipMalloc(&t->tailCount, 2 * sizeof(unsigned)));
+        MRT_HIP(hipMemset(t->tailCount, 0, 2 * sizeof(unsigned)));
+        MRT_HIP(hipMalloc(&t->tailRec, (size_t)mrt::kTailWords * kTailCapacity * sizeof(int)));
     }
     if (!t->evStart) {
         MRT_HIP(hipEventCreate(&t->evStart));
@@ -198,7 +220,19 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     int perCU = 0;
     const int blocks = grid_blocks(t, v, numRays, &perCU);
     const int totalLanes = blocks * mrt::kBlockThreads;
-    if (int rc = ensure_workspace(t, totalLanes, v.ldsStack)) return rc;
+    // Tail export / resume: while-while launches only. The resume pass uses at
+    // most the first pass's grid (so the spill slab fits both).
+    const bool tail = !v.ifif && t->cfg.tail_lanes > 0;
+    mrt::TraceVariant vr = v;
+    vr.resume = true;
+    int resumeBlocks = 0;
+    if (tail) {
+        int occ = t->occ[variant_key(vr)];
+        if (occ <= 0 && (mrt::trace_occupancy(vr, &occ) != hipSuccess || occ <= 0)) occ = 1;
+        t->occ[variant_key(vr)] = occ;
+        resumeBlocks = std::min(blocks, std::min(occ, t->cfg.tail_resume_waves / 4) * t->numCUs);
+    }
+    if (int rc = ensure_workspace(t, totalLanes, v.ldsStack, tail)) return rc;
 
     mrt::TraceArgs a{};
     a.rays = static_cast<const float4*>(rays);
@@ -217,6 +251,16 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     a.spill = t->spill;
     a.status = t->status;
     a.stats = reinterpret_cast<int4*>(stats);
+    if (tail) {
+        ++t->tailEpoch;
+        a.tailLanes = t->cfg.tail_lanes;
+        a.tailAfter = t->cfg.tail_after_us * 100;   // s_memrealtime runs at 100 MHz
+        a.tailResumeLanes = t->cfg.tail_resume_lanes;
+        a.tailCapacity = kTailCapacity;
+        a.tailCount = t->tailCount + (t->tailEpoch & 1u);
+        a.tailCountNext = t->tailCount + ((t->tailEpoch + 1u) & 1u);
+        a.tailRec = t->tailRec;
+    }
 
     hipStream_t s = static_cast<hipStream_t>(stream);
     // Queue heads restart at zero for every launch; strided mode has none.
@@ -224,6 +268,11 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
         MRT_HIP(hipMemsetAsync(t->queues, 0, mrt::kMaxQueues * mrt::kQueueStrideWords * sizeof(unsigned), s));
     if (info) MRT_HIP(hipEventRecord(t->evStart, s));
     MRT_HIP(mrt::launch_trace(v, a, blocks, s));
+    if (tail) {
+        mrt::TraceArgs r = a;
+        r.totalLanes = resumeBlocks * mrt::kBlockThreads;
+        MRT_HIP(mrt::launch_trace(vr, r, resumeBlocks, s));
+    }
     if (info) {
         MRT_HIP(hipEventRecord(t->evStop, s));
         MRT_HIP(hipEventSynchronize(t->evStop));
@@ -235,6 +284,11 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
         int overflow = 0;
         MRT_HIP(hipMemcpy(&overflow, t->status, sizeof(int), hipMemcpyDeviceToHost));
         info->stack_overflows = overflow;
+        if (tail) {
+            unsigned n = 0;
+            MRT_HIP(hipMemcpy(&n, a.tailCount, sizeof(n), hipMemcpyDeviceToHost));
+            info->tail_records = (int32_t)n;
+        }
     }
     return MRT_OK;
 }
@@ -333,6 +387,8 @@ int mrt_tracer_destroy(mrt_tracer* t) {
         if (t->queues) (void)hipFree(t->queues);
         if (t->status) (void)hipFree(t->status);
         if (t->spill) (void)hipFree(t->spill);
+        if (t->tailCount) (void)hipFree(t->tailCount);
+        if (t->tailRec) (void)hipFree(t->tailRec);
         if (t->evStart) (void)hipEventDestroy(t->evStart);
         if (t->evStop) (void)hipEventDestroy(t->evStop);
     }
@@ -378,6 +434,10 @@ int mrt_tracer_set_config(mrt_tracer* t, const mrt_launch_cfg* cfg) {
     if (c.lds_stack == 0) c.lds_stack = d.lds_stack;
     if (c.schedule == 0) c.schedule = d.schedule;
     if (c.lane_groups == 0) c.lane_groups = d.lane_groups;
+    if (c.tail_lanes == 0) c.tail_lanes = d.tail_lanes;
+    if (c.tail_after_us == 0) c.tail_after_us = d.tail_after_us;
+    if (c.tail_resume_lanes == 0) c.tail_resume_lanes = d.tail_resume_lanes;
+    if (c.tail_resume_waves == 0) c.tail_resume_waves = d.tail_resume_waves;
     if (!valid_cfg(c)) return fail(MRT_ERR_INVALID_ARG, "launch config out of range");
     std::lock_guard<std::mutex> lock(t->mu);
     t->cfg = c;

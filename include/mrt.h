@@ -75,6 +75,15 @@ typedef struct mrt_launch_cfg {
                                   divergent waves (profiles/round1_tuning.md). 0 = library default */
     int32_t lane_groups;       /* strided mode: a wave's 64 lanes take rays from this many (1..64, power of
                                   two) distant sub-ranges of the batch instead of 64 consecutive rays */
+    int32_t tail_lanes;        /* while-while only: a wave whose current round has run tail_after_us and is
+                                  down to at most this many (1..64) traversing lanes writes each lane's state
+                                  (ray, hit so far, node, stack) to a tail slab and drops it; a second launch
+                                  on the same stream resumes those lanes tail_resume_lanes per wave, spread
+                                  over all CUs. Results unchanged. -1 = off, 0 = library default */
+    int32_t tail_after_us;     /* see tail_lanes (1..100000 microseconds; 0 = library default)   */
+    int32_t tail_resume_lanes; /* see tail_lanes (1..64 lanes per resuming wave; 0 = library default) */
+    int32_t tail_resume_waves; /* see tail_lanes: resuming waves per CU (4..32, a multiple of 4; 0 = library
+                                  default). Few waves per CU give each resumed lane a SIMD of its own */
 } mrt_launch_cfg;
 
 /* Per-launch statistics reported back to the host (optional). */
@@ -85,6 +94,7 @@ typedef struct mrt_trace_info {
     int32_t lds_stack_entries; /* per-lane traversal-stack entries held in LDS                    */
     int32_t stack_overflows;   /* lanes that needed more than 64 stack entries (0 for SBVH depth<=64) */
     int32_t schedule;          /* traversal schedule the launch used (1 while-while, 2 if-if)     */
+    int32_t tail_records;      /* lanes exported to the tail resume pass (tail_lanes; 0 when off) */
 } mrt_trace_info;
 
 /* ---- handle API -------------------------------------------------------- */

@@ -219,6 +219,54 @@ def test_if_if_deep_stacks_and_rebinding(tracer):
         tracer.set_config(**saved)
 
 
+# ---------------------------------------------------------------- tail export / resume
+TAIL_CFGS = [dict(tail_lanes=64, tail_after_us=1), dict(tail_lanes=64, tail_after_us=1, tail_resume_lanes=64),
+             dict(tail_lanes=64, tail_after_us=1, lds_stack=8, tail_resume_lanes=3),
+             dict(tail_lanes=8, tail_after_us=2, waves_per_cu=4), dict(tail_lanes=64, tail_after_us=1, lane_groups=8),
+             dict(tail_lanes=64, tail_after_us=1, tail_resume_waves=4, tail_resume_lanes=2)]
+
+
+@pytest.mark.parametrize("cfg", TAIL_CFGS, ids=lambda c: ",".join(f"{k}={v}" for k, v in c.items()))
+@pytest.mark.parametrize("wl", WORKLOADS, ids=lambda w: "-".join(map(str, w)))
+def test_tail_export_resume_is_bit_identical(tracer, wl, cfg):
+    """Lanes exported mid-traversal (state + stack) and resumed by the second launch
+    give the oracle's results and per-ray counters exactly (per-lane order), and the
+    speculative mode's closest hits exactly; a 1-us threshold exports most lanes."""
+    bufs, rays, any_hit, want, st = scene_setup(*wl)
+    saved = tracer.config()
+    try:
+        tracer.set_config(**cfg)
+        res, gst = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=False, stats=True)
+        exported = tracer.last_info["tail_records"]
+        assert np.array_equal(res[:, :2], want[:, :2]) and np.array_equal(gst[:, :3], st[:, :3])
+        res2, _ = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=True)
+        if any_hit:
+            assert_valid_hits(rays, res2, want, bufs)
+        else:
+            assert np.array_equal(res2[:, :2], want[:, :2])
+        if cfg["tail_lanes"] == 64:
+            assert exported > 0, "the 1-us threshold exported nothing: the resume pass went untested"
+    finally:
+        tracer.set_config(**saved)
+
+
+def test_tail_counters_alternate_across_launches(tracer):
+    """Back-to-back exporting launches on one stream (the record counter of each is
+    zeroed by the previous one) and a launch with the tail off in between."""
+    bufs, rays, any_hit, want, _ = scene_setup("sponza", 256, 192, "diffuse")
+    saved = tracer.config()
+    try:
+        for cfg in (dict(tail_lanes=64, tail_after_us=1), dict(tail_lanes=-1), dict(tail_lanes=32, tail_after_us=1)):
+            tracer.set_config(**cfg)
+            for _ in range(3):
+                res, _ = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=True)
+                assert np.array_equal(res[:, :2], want[:, :2])
+                if cfg["tail_lanes"] < 0:
+                    assert tracer.last_info["tail_records"] == 0
+    finally:
+        tracer.set_config(**saved)
+
+
 def test_invalid_config_rejected(tracer):
     from mrt._lib import MrtError
     with pytest.raises(MrtError):
@@ -227,6 +275,10 @@ def test_invalid_config_rejected(tracer):
         tracer.set_config(num_queues=9)
     with pytest.raises(MrtError):
         tracer.set_config(schedule=3)
+    with pytest.raises(MrtError):
+        tracer.set_config(tail_lanes=65)
+    with pytest.raises(MrtError):
+        tracer.set_config(tail_resume_lanes=-2)
 
 
 # ---------------------------------------------------------------- edge cases

@@ -45,7 +45,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="bunny-primary-1024x768")
     ap.add_argument("--variant", action="append", required=True, help="libdir:json-config")
-    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--fast-rcp", action="store_true")
     args = ap.parse_args()
