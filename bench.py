@@ -50,6 +50,13 @@ REFERENCE_MRAYS = {
     "sponza-ao-640x480": 1022.61,
     "conference-diffuse-640x480": 831.28,
     "hairball-primary-640x480": 280.49,
+    "dragon-primary-640x480": 575.43,
+    "fairy-ao-640x480": 1280.77,
+    "fairy-diffuse-640x480": 678.77,
+    "sibenik-ao-640x480": 1499.86,
+    "sibenik-diffuse-640x480": 286.97,
+    "san-ao-640x480": 556.89,
+    "san-diffuse-640x480": 132.28,
 }
 
 WORKLOADS = {

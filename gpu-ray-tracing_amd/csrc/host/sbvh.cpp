@@ -14,6 +14,7 @@
 #include <chrono>
 #include <climits>
 #include <cmath>
+#include <cstdlib>
 #include <thread>
 
 #include "bvh.hpp"
@@ -137,7 +138,14 @@ private:
 class Builder {
 public:
     Builder(const Scene& s, const BuildParams& p) : sc_(s), p_(p) {
-        int threads = p.threads > 0 ? p.threads : (int)std::thread::hardware_concurrency();
+        // Default: OMP_NUM_THREADS when set (the GPU hosts export their CPU share
+        // there; hardware_concurrency() counts the whole machine), else all cores.
+        int threads = p.threads;
+        if (threads <= 0) {
+            const char* env = std::getenv("OMP_NUM_THREADS");
+            threads = env ? std::atoi(env) : 0;
+        }
+        if (threads <= 0) threads = (int)std::thread::hardware_concurrency();
         freeThreads_.store(std::max(0, threads - 1));
     }
 

@@ -122,7 +122,8 @@ def scene_setup(name, w, h, kind):
 
 
 WORKLOADS = [("bunny", 320, 240, "primary"), ("conference", 256, 192, "ao"), ("sponza", 256, 192, "diffuse"),
-             ("conference", 256, 192, "diffuse"), ("mori", 256, 192, "ao"), ("hairball:800", 256, 192, "diffuse")]
+             ("conference", 256, 192, "diffuse"), ("mori", 256, 192, "ao"), ("hairball:800", 256, 192, "diffuse"),
+             ("sibenik", 256, 192, "diffuse"), ("fairy", 256, 192, "ao"), ("dragon", 256, 192, "primary")]
 
 
 @pytest.mark.parametrize("wl", WORKLOADS, ids=lambda w: "-".join(map(str, w)))

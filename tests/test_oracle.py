@@ -127,3 +127,21 @@ def test_camera_matrix_export_reproduces_the_host_primary_rays(jx, jy):
     inv = (f(1) * (f(1) / np.sqrt(dd))).astype(f)
     dirs = (d * inv[:, None]).astype(f)
     assert np.array_equal(dirs.view(np.uint32), rays[:, 4:7].view(np.uint32))
+
+
+@pytest.mark.parametrize("scene_name,tris", [("mori", 12570), ("bunny", 144500), ("sponza", 121384),
+                                             ("conference", 350949), ("dragon", 910348), ("fairy", 174117),
+                                             ("sibenik", 75284)])
+def test_stand_in_scenes_have_their_triangle_counts(scene_name, tris):
+    """README.md:48-58 counts (fairy/sibenik: commonly distributed sizes, the README gives none)."""
+    assert mrt.Scene.synthetic(scene_name, 0, 1).num_triangles == tris
+
+
+def test_closed_nave_stand_in_hits_every_primary_ray():
+    """The sibenik stand-in is a closed interior: diffuse rays from it never escape (README diffuse row)."""
+    scene = mrt.Scene.synthetic("sibenik", 0, 1)
+    nodes, woop, tri = mrt.Bvh.build(scene).buffers()
+    cam, _ = scene.camera()
+    rays, _ = mrt.primary_rays(cam, 48, 36)
+    res, _, _ = O.trace(rays, nodes, woop, tri, threads=4)
+    assert (res[:, 0] != -1).all()

@@ -1,0 +1,126 @@
+"""Every scene x ray-type cell of the reference's README performance table
+(README.md:60-81) measured on one MI355X with bench.py's workload code, next to
+the README's Kepler Mrays/s.
+
+Same measurement as bench.py (exact-rcp production kernel, device-generated
+rays, rays counted / kernel time of the timed steps); per cell also the
+oracle's agreement on the first `--parity-rays` rays of the batch (closest
+hit: id and t bit-identical; any hit: hit/miss identical). Scenes are the
+deterministic stand-ins of csrc/host/scene.cpp; fairy, sibenik and san have no
+size in the README (their commonly distributed triangle counts are assumed).
+
+  python tools/readme_table.py [--bvh-cache DIR] [--steps K] [--cells a,b,...]
+
+Writes gpurun_out/readme_table.json and gpurun_out/readme_table.md.
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "gpu-ray-tracing_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+# README rows in table order: (workload, README Mrays/s, README line).
+CELLS = [
+    ("sponza-primary-640x480", 597.51, 61), ("mori-primary-640x480", 1271.61, 62),
+    ("hairball-primary-640x480", 280.49, 63), ("dragon-primary-640x480", 575.43, 64),
+    ("bunny-primary-640x480", 825.11, 65),
+    ("conference-diffuse-640x480", 831.28, 68), ("fairy-diffuse-640x480", 678.77, 69),
+    ("sibenik-diffuse-640x480", 286.97, 70), ("san-diffuse-640x480", 132.28, 71),
+    ("sponza-diffuse-640x480", 325.33, 72), ("mori-diffuse-640x480", 1466.05, 73),
+    ("conference-ao-640x480", 1478.43, 76), ("fairy-ao-640x480", 1280.77, 77),
+    ("sibenik-ao-640x480", 1499.86, 78), ("san-ao-640x480", 556.89, 79),
+    ("sponza-ao-640x480", 1022.61, 80), ("mori-ao-640x480", 2763.01, 81),
+]
+
+
+def heartbeat(stop, state):
+    # The GPU pool takes 3 silent minutes for a hang; the big SBVH builds are long and quiet.
+    while not stop.wait(30):
+        print(f"  ... {state['cell']} ({time.perf_counter() - state['t0']:.0f} s)", file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--bvh-cache", default="/tmp/mrt_bvhcache")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--parity-rays", type=int, default=16384)
+    ap.add_argument("--cells", default="", help="comma-separated subset of workloads")
+    ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out"))
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import bench
+    import oracle_lib as O
+    from mrt.tracer import Tracer
+
+    torch.cuda.set_device(0)
+    tracer = Tracer(0)
+    want = set(args.cells.split(",")) if args.cells else None
+    state = {"cell": "start", "t0": time.perf_counter()}
+    stop = threading.Event()
+    threading.Thread(target=heartbeat, args=(stop, state), daemon=True).start()
+    rows = []
+    for name, readme, line in CELLS:
+        if want and name not in want:
+            continue
+        state.update(cell=name, t0=time.perf_counter())
+        scene_name = bench.workload_spec(name)[0]
+        scene, bufs, bstats, build_s = bench.bvh_for(scene_name, 1, 0, args.bvh_cache)
+        batches = bench.Batches(name, scene, bufs, tracer)
+        alg_bytes, n_nodes, n_tris, n_leaves = bench.algorithmic_bytes(tracer, batches)
+        wall, launch_ms = bench.time_steps(tracer, batches, args.steps, args.warmup, 1, True)
+        value = batches.rays_counted * args.steps / wall / 1e6
+        kernel_ms = launch_ms * len(batches.batches)
+        # Parity on a prefix of the (first) batch against the oracle.
+        rb, _ = batches.batches[0]
+        n = min(args.parity_rays, rb.size)
+        rays = rb.rays.cpu().numpy()[:n]
+        gpu = rb.results_numpy()[:n]
+        any_hit = not rb.need_closest_hit
+        ref, _, _ = O.trace(rays, *bufs, any_hit=any_hit, threads=min(16, os.cpu_count() or 1))
+        if any_hit:
+            agree = float(((gpu[:, 0] == -1) == (ref[:, 0] == -1)).mean())
+        else:
+            agree = float(((gpu[:, 0] == ref[:, 0]) & (gpu[:, 1] == ref[:, 1])).mean())
+        row = {
+            "workload": name, "readme_mrays": readme, "readme_line": line,
+            "mrays": round(value, 2), "x_readme": round(value / readme, 2),
+            "kernel_ms": round(kernel_ms, 4), "rays_counted": batches.rays_counted, "rays_traced": batches.rays_traced,
+            "tris": scene.num_triangles, "inner_nodes": len(bufs[0]) // 16,
+            "bvh_mb": round(4 * (len(bufs[0]) + len(bufs[1]) + len(bufs[2])) / 2**20, 1), "build_s": round(build_s, 1),
+            "per_ray": {"nodes": round(n_nodes / batches.rays_traced, 2), "tris": round(n_tris / batches.rays_traced, 2)},
+            "alg_gbs": round(alg_bytes / (kernel_ms * 1e-3) / 1e9, 1),
+            "parity_rays": n, "parity_agree": agree, "parity_kind": "hit/miss" if any_hit else "id+t exact",
+        }
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+        del batches, bufs, scene
+        torch.cuda.empty_cache()
+    stop.set()
+
+    os.makedirs(args.out, exist_ok=True)
+    with open(os.path.join(args.out, "readme_table.json"), "w") as f:
+        json.dump(rows, f, indent=1)
+    md = ["| README cell | tris (stand-in) | inner nodes | README Mrays/s | MI355X Mrays/s | × README | kernel ms | "
+          "nodes/ray | tris/ray | alg. GB/s | oracle agreement |",
+          "|---|---|---|---|---|---|---|---|---|---|---|"]
+    for r in rows:
+        md.append(f"| {r['workload']} (README:{r['readme_line']}) | {r['tris']:,} | {r['inner_nodes']:,} | {r['readme_mrays']} | "
+                  f"**{r['mrays']}** | {r['x_readme']} | {r['kernel_ms']} | {r['per_ray']['nodes']} | "
+                  f"{r['per_ray']['tris']} | {r['alg_gbs']} | {r['parity_agree']:.4f} ({r['parity_kind']}, "
+                  f"{r['parity_rays']} rays) |")
+    with open(os.path.join(args.out, "readme_table.md"), "w") as f:
+        f.write("\n".join(md) + "\n")
+    print("\n".join(md))
+
+
+if __name__ == "__main__":
+    main()
