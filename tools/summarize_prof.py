@@ -27,7 +27,7 @@ for p in sorted(d for d in os.listdir(src) if d.startswith("pmc")):
     for r in rows:
         if r["Kernel_Name"] == timed["Name"]:
             vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-            grid = {"grid_size": int(r["Grid_Size"]), "vgpr": int(r["VGPR_Count"]), "lds": int(r["LDS_Block_Size"])}
+            grid = {"grid_size": int(r["Grid_Size"]), "rocprof_VGPR_Count_field": int(r["VGPR_Count"]), "lds": int(r["LDS_Block_Size"])}
     for k, v in vals.items():
         out["pmc"][k] = {"per_launch_mean": sum(v) / len(v), "launches": len(v)}
     out.update(grid)
