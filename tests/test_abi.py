@@ -70,3 +70,18 @@ def test_ctypes_structs_match_the_header(struct, cls):
     body = re.search(r"typedef struct " + struct + r"\s*\{(.*?)\}\s*" + struct + ";", text, flags=re.S).group(1)
     fields = re.findall(r"\b(?:int32_t|float)\s+([A-Za-z_][A-Za-z0-9_]*)\s*;", body)
     assert fields == [n for n, _ in cls._fields_]
+
+
+def test_cpp_dropin_resolves_the_reference_prototypes_from_libmrt():
+    """tests/cpp/cuda_tracer_dropin.cpp declares CudaTracerKernels.hh:42-52 with the
+    reference's own parameter types; its undefined symbols are exactly those four
+    names (C linkage, no mangling) and libmrt.so resolves them at load time."""
+    import subprocess
+    exe = os.path.join(REPO, "gpu-ray-tracing_amd", "lib", "cuda_tracer_dropin")
+    if not os.path.exists(exe):
+        pytest.skip("not built (make -C gpu-ray-tracing_amd)")
+    undef = subprocess.run(["nm", "-D", "--undefined-only", exe], capture_output=True, text=True, check=True).stdout
+    wanted = {"bind_CudaBVHTexture", "unbind_CudaBVHTexture", "launch_tracingKernel", "copy_tracing_results"}
+    assert wanted <= set(line.split()[-1] for line in undef.splitlines() if line.strip())
+    ldd = subprocess.run(["ldd", exe], capture_output=True, text=True, check=True).stdout
+    assert "libmrt.so" in ldd and "not found" not in ldd.split("libmrt.so", 1)[1].splitlines()[0]

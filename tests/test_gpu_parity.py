@@ -24,6 +24,7 @@ import mrt  # noqa: E402
 import oracle_lib as O  # noqa: E402
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.fixture(scope="module")
@@ -341,6 +342,35 @@ def test_reference_compat_entry_points(tracer):
     assert np.array_equal(host[:, 0], want[:, 0])
     assert ulp_diff(host[:, 1], want[:, 1]).max() <= 2
     lib.unbind_CudaBVHTexture()
+
+
+@pytest.mark.parametrize("wl", [("bunny", 320, 240, "primary"), ("conference", 256, 192, "ao")],
+                         ids=lambda w: "-".join(map(str, w)))
+def test_cpp_host_links_reference_prototypes(tmp_path, wl):
+    """A C++ CudaTracer written against the reference's CudaTracerKernels.hh:42-52
+    prototypes (tests/cpp/cuda_tracer_dropin.cpp), linked to libmrt.so, run as a
+    child process: the reference's host side works unchanged on top of the library."""
+    import subprocess
+    exe = os.path.join(REPO, "gpu-ray-tracing_amd", "lib", "cuda_tracer_dropin")
+    assert os.path.exists(exe), "build it: make -C gpu-ray-tracing_amd"
+    bufs, rays, any_hit, want, _ = scene_setup(*wl)
+    names = []
+    for name, arr in zip(("nodes", "woop", "tri", "rays"), (*bufs, rays)):
+        path = tmp_path / f"{name}.bin"
+        np.ascontiguousarray(arr).tofile(path)
+        names.append(str(path))
+    out = tmp_path / "results.bin"
+    r = subprocess.run([exe, *names, str(int(any_hit)), str(out)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    got = np.fromfile(out, np.int32).reshape(-1, 4)
+    assert len(got) == len(rays)
+    # launch_tracingKernel keeps the reference's fast reciprocal (rcp.approx there, v_rcp_f32 here).
+    if any_hit:
+        assert np.array_equal(got[:, 0] == -1, want[:, 0] == -1)
+    else:
+        assert np.array_equal(got[:, 0], want[:, 0])
+        assert ulp_diff(got[:, 1], want[:, 1]).max() <= 2
+    assert not got[:, 2:].any()   # RayResult pads untouched
 
 
 def test_async_trace_on_a_side_stream(tracer):
