@@ -95,7 +95,7 @@ EXTRA_N1 = ["bunny-primary-640x480", "conference-ao-640x480", "sponza-diffuse-64
 # cannot be read inside this timed process, so the committed profile is cited.
 PMC_PROFILES = {w: f"profiles/round1_{w}_pmc_summary.json" for w in
                 ("bunny-primary-1024x768", "bunny-primary-640x480", "conference-ao-640x480", "sponza-diffuse-640x480",
-                 "hairball-diffuse-640x480")}
+                 "sponza-diffuse2-640x480", "hairball-diffuse-640x480")}
 
 
 def pmc_traffic(name):
