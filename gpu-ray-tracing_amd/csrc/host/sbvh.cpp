@@ -2,8 +2,9 @@
 //
 // Restates the reference's SplitBVHBuilder (src/rt/bvh/SplitBVHBuilder.cc:55-485,
 // Stich et al. 2009) including the parts that decide output bits: the
-// reference's median-3 quicksort + insertion sort (src/framework/base/Sort.cc:
-// 63-239) with the (centroid sum, triIdx) comparator, the SAH tie-break on
+// order of the reference's median-3 quicksort (src/framework/base/Sort.cc:
+// 63-239) with the (centroid sum, triIdx) comparator — a strict total order
+// within a node, so std::sort reproduces it — the SAH tie-break on
 // i^2 + (n-i)^2, degenerate-reference removal by swap-with-last, the 128-bin
 // spatial search with float->int bin truncation, and the duplicate / unsplit
 // decision. Where the reference kept one global reference stack and built the
@@ -15,6 +16,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <thread>
 
 #include "bvh.hpp"
@@ -27,6 +29,8 @@ constexpr int kMaxDepth = 64;          // SplitBVHBuilder.hh:41-45
 constexpr int kMaxSpatialDepth = 48;
 constexpr int kNumSpatialBins = 128;
 constexpr int kParallelMinRefs = 8192; // subtrees at least this large may run on their own thread
+constexpr int kParallelSortRefs = 65536; // nodes at least this large sort their three axes concurrently
+constexpr size_t kRadixSortRefs = 4096;  // nodes at least this large radix-sort their references
 
 struct Ref {
     int32_t triIdx = -1;
@@ -62,78 +66,49 @@ inline int trunc_to_int(float x) {
 inline int clampi(int v, int lo, int hi) { return std::min(std::max(v, lo), hi); }
 
 // FW::sort over a Ref array ordered by (min+max)[dim], then triIdx
-// (SplitBVHBuilder.cc:75-84 with Sort.cc:63-239).
-class RefSorter {
-public:
-    RefSorter(std::vector<Ref>& r, int dim) : refs_(r), dim_(dim) {}
-
-    void sort(int start, int end) {
-        if (end - start < 2) return;
-        qsort(start, end);
+// (SplitBVHBuilder.cc:75-84 with Sort.cc:63-239). Within one node every
+// triangle has at most one reference (a spatial split sends a duplicated
+// triangle's two halves to different children), so (key, triIdx) is a strict
+// total order and the sorted permutation is unique: std::sort returns exactly
+// the reference's median-3 quicksort result (checked by the builder's golden
+// Compact2 fixtures and the per-scene hashes in tests/test_oracle.py).
+void sort_refs(std::vector<Ref>& refs, int dim) {
+    // The same order as 64-bit integer keys — the float key's order-preserving
+    // bits (-0 folded into +0, which compares equal to it), then triIdx — with
+    // the position as payload: 16-B records sort far faster than 28-B Refs with a
+    // float add per compare. Large nodes: LSD radix sort (16-bit digits, passes
+    // whose digit is constant skipped); small ones: std::sort.
+    struct KeyPos { uint64_t key; uint32_t pos; };
+    const size_t n = refs.size();
+    if (n < 2) return;
+    std::vector<KeyPos> a(n);
+    for (size_t i = 0; i < n; i++) {
+        float c = refs[i].bounds.mn[dim] + refs[i].bounds.mx[dim];
+        c = c + 0.0f;   // -0 -> +0
+        uint32_t u;
+        std::memcpy(&u, &c, 4);
+        u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+        a[i] = {((uint64_t)u << 32) | (uint32_t)refs[i].triIdx, (uint32_t)i};
     }
-
-private:
-    bool less(int a, int b) const {
-        const Ref& ra = refs_[a];
-        const Ref& rb = refs_[b];
-        const float ca = ra.bounds.mn[dim_] + ra.bounds.mx[dim_];
-        const float cb = rb.bounds.mn[dim_] + rb.bounds.mx[dim_];
-        return ca < cb || (ca == cb && ra.triIdx < rb.triIdx);
-    }
-    void swp(int a, int b) { std::swap(refs_[a], refs_[b]); }
-
-    void insertion_sort(int start, int size) {
-        for (int i = 1; i < size; i++) {
-            int j = start + i - 1;
-            while (j >= start && less(j + 1, j)) {
-                swp(j, j + 1);
-                j--;
-            }
+    if (n < kRadixSortRefs) {
+        std::sort(a.begin(), a.end(), [](const KeyPos& x, const KeyPos& y) { return x.key < y.key; });
+    } else {
+        std::vector<KeyPos> b(n);
+        std::vector<uint32_t> count(1 << 16);
+        for (int shift = 0; shift < 64; shift += 16) {
+            std::fill(count.begin(), count.end(), 0u);
+            for (size_t i = 0; i < n; i++) count[(a[i].key >> shift) & 0xFFFF]++;
+            if (count[(a[0].key >> shift) & 0xFFFF] == n) continue;   // one digit value: the pass is the identity
+            uint32_t sum = 0;
+            for (uint32_t& c : count) { const uint32_t t = c; c = sum; sum += t; }
+            for (size_t i = 0; i < n; i++) b[count[(a[i].key >> shift) & 0xFFFF]++] = a[i];
+            a.swap(b);
         }
     }
-    int median3(int low, int high) const {
-        int l = low;
-        int c = (low + high) >> 1;
-        int h = high - 2;
-        if (less(h, l)) std::swap(l, h);
-        if (less(c, l)) c = l;
-        return less(h, c) ? h : c;
-    }
-    int partition(int low, int high) {
-        swp(median3(low, high), high - 1);
-        int i = low - 1;
-        int j = high - 1;
-        for (;;) {
-            do i++; while (less(i, high - 1));
-            do j--; while (less(high - 1, j));
-            if (i >= j) break;
-            swp(i, j);
-        }
-        swp(i, high - 1);
-        return i;
-    }
-    void qsort(int low, int high) {
-        constexpr int kStack = 32, kMin = 16;
-        int stack[kStack];
-        int sp = 0;
-        stack[sp++] = high;
-        while (sp) {
-            high = stack[--sp];
-            if (high - low < kMin || sp + 2 > kStack) {
-                insertion_sort(low, high - low);
-                low = high + 1;
-                continue;
-            }
-            const int i = partition(low, high);
-            if (high - i > 2) stack[sp++] = high;
-            if (i - low > 1) stack[sp++] = i;
-            else low = i + 1;
-        }
-    }
-
-    std::vector<Ref>& refs_;
-    int dim_;
-};
+    std::vector<Ref> out(n);
+    for (size_t i = 0; i < n; i++) out[i] = refs[a[i].pos];
+    refs.swap(out);
+}
 
 class Builder {
 public:
@@ -249,16 +224,31 @@ private:
         const int n = (int)refs.size();
         float bestTieBreak = FLT_MAX;
         std::vector<AABB> rightBounds(std::max(n - 1, 1));
+        // The order is unique, so the three axes sort independently: large nodes
+        // (the serial top of the tree) sort x and y on copies on their own threads
+        // while z sorts `refs` in place, as the sequential loop leaves it.
+        const bool par = n >= kParallelSortRefs;
+        std::vector<Ref> byDim[2];
+        if (par) {
+            byDim[0] = refs;
+            byDim[1] = refs;
+            std::thread tx([&] { sort_refs(byDim[0], 0); });
+            std::thread ty([&] { sort_refs(byDim[1], 1); });
+            sort_refs(refs, 2);
+            tx.join();
+            ty.join();
+        }
         for (int dim = 0; dim < 3; dim++) {
-            RefSorter(refs, dim).sort(0, n);
+            if (!par) sort_refs(refs, dim);
+            const std::vector<Ref>& sorted = (par && dim < 2) ? byDim[dim] : refs;
             AABB rb;
             for (int i = n - 1; i > 0; i--) {
-                rb.grow(refs[i].bounds);
+                rb.grow(sorted[i].bounds);
                 rightBounds[i - 1] = rb;
             }
             AABB lb;
             for (int i = 1; i < n; i++) {
-                lb.grow(refs[i - 1].bounds);
+                lb.grow(sorted[i - 1].bounds);
                 const float sah = nodeSAH + lb.area() * tri_cost(i) + rightBounds[i - 1].area() * tri_cost(n - i);
                 const float tieBreak = (float)i * (float)i + (float)(n - i) * (float)(n - i);
                 if (sah < split.sah || (sah == split.sah && tieBreak < bestTieBreak)) {
@@ -277,7 +267,7 @@ private:
     // performObjectSplit (:235-245).
     void perform_object_split(NodeSpec& left, NodeSpec& right, std::vector<Ref>& refs, const NodeSpec& spec,
                               const ObjectSplit& split) const {
-        RefSorter(refs, split.sortDim).sort(0, (int)refs.size());
+        sort_refs(refs, split.sortDim);
         left.numRef = split.numLeft;
         left.bounds = split.leftBounds;
         right.numRef = spec.numRef - split.numLeft;
