@@ -145,3 +145,13 @@ def test_closed_nave_stand_in_hits_every_primary_ray():
     rays, _ = mrt.primary_rays(cam, 48, 36)
     res, _, _ = O.trace(rays, nodes, woop, tri, threads=4)
     assert (res[:, 0] != -1).all()
+
+
+@pytest.mark.parametrize("scene_name,digest", [("conference", "dfbbbfea18d11fba"), ("sponza", "c7e34a6a5c968e5e"),
+                                               ("bunny", "a030c6170e26b859")])
+def test_builder_output_is_pinned(scene_name, digest):
+    """SHA-256 (prefix) of the Compact2 bytes of three stand-ins: the builder's output must not move when its
+    internals do (the sort, the threading). Regression pin of this repo's builder, not a reference output."""
+    import hashlib
+    nodes, woop, tri = mrt.Bvh.build(mrt.Scene.synthetic(scene_name, 0, 1)).buffers()
+    assert hashlib.sha256(nodes.tobytes() + woop.tobytes() + tri.tobytes()).hexdigest()[:16] == digest
