@@ -12,6 +12,7 @@
 // of the segment it owns, which yields the same subtree bits and lets large
 // subtrees build on separate threads.
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <climits>
 #include <cmath>
@@ -28,8 +29,7 @@ namespace {
 constexpr int kMaxDepth = 64;          // SplitBVHBuilder.hh:41-45
 constexpr int kMaxSpatialDepth = 48;
 constexpr int kNumSpatialBins = 128;
-constexpr int kParallelMinRefs = 8192; // subtrees at least this large may run on their own thread
-constexpr int kParallelSortRefs = 65536; // nodes at least this large sort their three axes concurrently
+constexpr int kParallelMinRefs = 1024; // subtrees at least this large may run on their own thread
 constexpr size_t kRadixSortRefs = 4096;  // nodes at least this large radix-sort their references
 
 struct Ref {
@@ -110,6 +110,8 @@ void sort_refs(std::vector<Ref>& refs, int dim) {
     refs.swap(out);
 }
 
+using Axes = std::array<std::vector<Ref>, 3>;
+
 class Builder {
 public:
     Builder(const Scene& s, const BuildParams& p) : sc_(s), p_(p) {
@@ -135,7 +137,20 @@ public:
         }
         root.numRef = (int)refs.size();
         minOverlap_ = root.bounds.area() * p_.splitAlpha;
-        return build(std::move(refs), root, 0);
+        numTris_ = sc_.triangles.size();
+        // The node's references sorted along each axis, kept through the splits
+        // (a subset of a uniquely ordered array is ordered): three sorts in total
+        // instead of four per node.
+        Axes axes;
+        for (int d = 0; d < 3; d++) axes[d] = refs;
+        {
+            std::thread tx([&] { sort_refs(axes[0], 0); });
+            std::thread ty([&] { sort_refs(axes[1], 1); });
+            sort_refs(axes[2], 2);
+            tx.join();
+            ty.join();
+        }
+        return build(std::move(refs), std::move(axes), root, 0);
     }
 
 private:
@@ -148,23 +163,33 @@ private:
 
     // SplitBVHBuilder.cc:113-174. `refs` is exactly the node's segment of the
     // reference's m_refStack, in the same order.
-    std::unique_ptr<BvhNode> build(std::vector<Ref> refs, NodeSpec spec, int level) {
+    std::unique_ptr<BvhNode> build(std::vector<Ref> refs, Axes axes, NodeSpec spec, int level) {
         // Remove degenerates (:120-129).
+        std::vector<int32_t> removed;
         for (int i = (int)refs.size() - 1; i >= 0; i--) {
             const Vec3f size = refs[i].bounds.mx - refs[i].bounds.mn;
             if (size.min_comp() < 0.0f || size.sum() == size.max_comp()) {
+                removed.push_back(refs[i].triIdx);
                 refs[i] = refs.back();
                 refs.pop_back();
             }
         }
         spec.numRef = (int)refs.size();
+        if (!removed.empty()) {   // the same references leave the sorted arrays (triIdx is unique in a node)
+            std::vector<uint8_t>& mark = marks();
+            for (int32_t t : removed) mark[t] = 1;
+            for (auto& a : axes)
+                a.erase(std::remove_if(a.begin(), a.end(), [&](const Ref& r) { return mark[r.triIdx] != 0; }), a.end());
+            for (int32_t t : removed) mark[t] = 0;
+        }
 
         if (spec.numRef <= p_.minLeafSize || level >= kMaxDepth) return make_leaf(refs, spec);
 
         const float area = spec.bounds.area();
         const float leafSAH = area * tri_cost(spec.numRef);
         const float nodeSAH = area * node_cost(2);
-        const ObjectSplit object = find_object_split(refs, nodeSAH);
+        const ObjectSplit object = find_object_split(axes, nodeSAH);
+        refs = axes[2];   // the reference's sweeps leave the node's references sorted along z
 
         SpatialSplit spatial;
         if (level < kMaxSpatialDepth) {
@@ -178,21 +203,27 @@ private:
 
         NodeSpec left, right;
         if (minSAH == spatial.sah) perform_spatial_split(left, right, refs, spatial);
-        if (!left.numRef || !right.numRef) perform_object_split(left, right, refs, spec, object);
+        if (!left.numRef || !right.numRef) {
+            perform_object_split(left, right, refs, spec, object);
+            refs = axes[object.sortDim];   // the sort's result: the node's references are the same set
+        }
 
         std::vector<Ref> rightRefs(refs.begin() + left.numRef, refs.end());
         refs.resize(left.numRef);
+        Axes leftAxes, rightAxes;
+        split_axes(axes, refs, rightRefs, leftAxes, rightAxes);
+        axes = Axes();
 
         auto node = std::make_unique<BvhNode>();
         node->bounds = spec.bounds;
         std::unique_ptr<BvhNode> rightNode;
         std::thread worker;
         if (right.numRef >= kParallelMinRefs && left.numRef >= kParallelMinRefs && take_thread()) {
-            worker = std::thread([&, lvl = level + 1] { rightNode = build(std::move(rightRefs), right, lvl); });
+            worker = std::thread([&, lvl = level + 1] { rightNode = build(std::move(rightRefs), std::move(rightAxes), right, lvl); });
         } else {
-            rightNode = build(std::move(rightRefs), right, level + 1);
+            rightNode = build(std::move(rightRefs), std::move(rightAxes), right, level + 1);
         }
-        std::unique_ptr<BvhNode> leftNode = build(std::move(refs), left, level + 1);
+        std::unique_ptr<BvhNode> leftNode = build(std::move(refs), std::move(leftAxes), left, level + 1);
         if (worker.joinable()) {
             worker.join();
             freeThreads_.fetch_add(1);
@@ -218,29 +249,15 @@ private:
         return leaf;
     }
 
-    // findObjectSplit (:191-231): three full sorts, right-to-left bound sweep.
-    ObjectSplit find_object_split(std::vector<Ref>& refs, float nodeSAH) const {
+    // findObjectSplit (:191-231): per axis, a right-to-left bound sweep over the
+    // references in sorted order (kept sorted through the splits, see run()).
+    ObjectSplit find_object_split(const Axes& axes, float nodeSAH) const {
         ObjectSplit split;
-        const int n = (int)refs.size();
+        const int n = (int)axes[0].size();
         float bestTieBreak = FLT_MAX;
         std::vector<AABB> rightBounds(std::max(n - 1, 1));
-        // The order is unique, so the three axes sort independently: large nodes
-        // (the serial top of the tree) sort x and y on copies on their own threads
-        // while z sorts `refs` in place, as the sequential loop leaves it.
-        const bool par = n >= kParallelSortRefs;
-        std::vector<Ref> byDim[2];
-        if (par) {
-            byDim[0] = refs;
-            byDim[1] = refs;
-            std::thread tx([&] { sort_refs(byDim[0], 0); });
-            std::thread ty([&] { sort_refs(byDim[1], 1); });
-            sort_refs(refs, 2);
-            tx.join();
-            ty.join();
-        }
         for (int dim = 0; dim < 3; dim++) {
-            if (!par) sort_refs(refs, dim);
-            const std::vector<Ref>& sorted = (par && dim < 2) ? byDim[dim] : refs;
+            const std::vector<Ref>& sorted = axes[dim];
             AABB rb;
             for (int i = n - 1; i > 0; i--) {
                 rb.grow(sorted[i].bounds);
@@ -264,10 +281,61 @@ private:
         return split;
     }
 
+    // The children's sorted arrays. A reference that went to one side whole keeps
+    // its bounds, hence its key, and its place in each parent array (a stable
+    // partition); the two clipped halves of a duplicated triangle get new keys
+    // and are sorted in and merged.
+    void split_axes(const Axes& axes, const std::vector<Ref>& leftRefs, const std::vector<Ref>& rightRefs,
+                    Axes& leftAxes, Axes& rightAxes) {
+        std::vector<uint8_t>& mark = marks();   // bit 0: on the left, bit 1: on the right
+        for (const Ref& r : leftRefs) mark[r.triIdx] |= 1;
+        for (const Ref& r : rightRefs) mark[r.triIdx] |= 2;
+        std::vector<Ref> dupLeft, dupRight;
+        for (const Ref& r : leftRefs)
+            if (mark[r.triIdx] == 3) dupLeft.push_back(r);
+        for (const Ref& r : rightRefs)
+            if (mark[r.triIdx] == 3) dupRight.push_back(r);
+        for (int d = 0; d < 3; d++) {
+            std::vector<Ref> l, rr;
+            l.reserve(leftRefs.size());
+            rr.reserve(rightRefs.size());
+            for (const Ref& r : axes[d]) {
+                const uint8_t m = mark[r.triIdx];
+                if (m == 1) l.push_back(r);
+                else if (m == 2) rr.push_back(r);
+            }
+            merge_sorted(l, dupLeft, d, leftAxes[d]);
+            merge_sorted(rr, dupRight, d, rightAxes[d]);
+        }
+        for (const Ref& r : leftRefs) mark[r.triIdx] = 0;
+        for (const Ref& r : rightRefs) mark[r.triIdx] = 0;
+    }
+
+    static void merge_sorted(std::vector<Ref>& base, std::vector<Ref> extra, int dim, std::vector<Ref>& out) {
+        if (extra.empty()) {
+            out = std::move(base);
+            return;
+        }
+        sort_refs(extra, dim);
+        out.resize(base.size() + extra.size());
+        std::merge(base.begin(), base.end(), extra.begin(), extra.end(), out.begin(), [dim](const Ref& a, const Ref& b) {
+            const float ca = a.bounds.mn[dim] + a.bounds.mx[dim];
+            const float cb = b.bounds.mn[dim] + b.bounds.mx[dim];
+            return ca < cb || (ca == cb && a.triIdx < b.triIdx);
+        });
+    }
+
+    // Per-thread scratch indexed by triIdx, all zero between uses.
+    std::vector<uint8_t>& marks() {
+        thread_local std::vector<uint8_t> m;
+        if (m.size() < numTris_) m.assign(numTris_, 0);
+        return m;
+    }
+
     // performObjectSplit (:235-245).
     void perform_object_split(NodeSpec& left, NodeSpec& right, std::vector<Ref>& refs, const NodeSpec& spec,
                               const ObjectSplit& split) const {
-        sort_refs(refs, split.sortDim);
+        (void)refs;   // the node's references sorted along split.sortDim are the caller's axes[sortDim]
         left.numRef = split.numLeft;
         left.bounds = split.leftBounds;
         right.numRef = spec.numRef - split.numLeft;
@@ -417,6 +485,7 @@ private:
     const Scene& sc_;
     const BuildParams& p_;
     float minOverlap_ = 0.0f;
+    size_t numTris_ = 0;
     std::atomic<int> freeThreads_{0};
 };
 
