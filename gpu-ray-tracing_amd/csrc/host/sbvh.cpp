@@ -31,6 +31,8 @@ constexpr int kMaxSpatialDepth = 48;
 constexpr int kNumSpatialBins = 128;
 constexpr int kParallelMinRefs = 1024; // subtrees at least this large may run on their own thread
 constexpr size_t kRadixSortRefs = 4096;  // nodes at least this large radix-sort their references
+constexpr int kParallelBinRefs = 32768;  // nodes at least this large bin their spatial-split search on threads
+constexpr int kBinThreads = 4;
 
 struct Ref {
     int32_t triIdx = -1;
@@ -55,6 +57,7 @@ struct SpatialBin {
     AABB bounds;
     int enter = 0;
     int exit = 0;
+    bool grown = false;   // bounds.grow() was called (an empty AABB grown in turns the bin infinite, as in the reference)
 };
 
 // (S32) of a float as x86-64 cvttss2si computes it: truncation, and the
@@ -348,30 +351,60 @@ private:
         const Vec3f binSize = (spec.bounds.mx - origin) * (1.0f / (float)kNumSpatialBins);
         const Vec3f invBinSize(1.0f / binSize.x, 1.0f / binSize.y, 1.0f / binSize.z);
 
-        std::vector<SpatialBin> bins(3 * kNumSpatialBins);
-        auto bin = [&](int dim, int i) -> SpatialBin& { return bins[dim * kNumSpatialBins + i]; };
-
-        for (const Ref& ref : refs) {
-            const Vec3f lo = (ref.bounds.mn - origin) * invBinSize;
-            const Vec3f hi = (ref.bounds.mx - origin) * invBinSize;
-            int firstBin[3], lastBin[3];
-            for (int d = 0; d < 3; d++) {
-                firstBin[d] = clampi(trunc_to_int(lo[d]), 0, kNumSpatialBins - 1);
-                lastBin[d] = clampi(trunc_to_int(hi[d]), firstBin[d], kNumSpatialBins - 1);
-            }
-            for (int dim = 0; dim < 3; dim++) {
-                Ref curr = ref;
-                for (int i = firstBin[dim]; i < lastBin[dim]; i++) {
-                    Ref l, r;
-                    split_reference(l, r, curr, dim, origin[dim] + binSize[dim] * (float)(i + 1));
-                    bin(dim, i).bounds.grow(l.bounds);
-                    curr = r;
+        // Binning (the search's cost: one splitReference per bin plane a reference
+        // crosses). Bin bounds are min/max unions and the counts sums, so any
+        // partition of the references gives the same bins: large nodes bin in
+        // chunks on their own threads and merge.
+        auto bin_refs = [&](size_t begin, size_t end, std::vector<SpatialBin>& out) {
+            out.assign(3 * kNumSpatialBins, SpatialBin());
+            for (size_t k = begin; k < end; k++) {
+                const Ref& ref = refs[k];
+                const Vec3f lo = (ref.bounds.mn - origin) * invBinSize;
+                const Vec3f hi = (ref.bounds.mx - origin) * invBinSize;
+                int firstBin[3], lastBin[3];
+                for (int d = 0; d < 3; d++) {
+                    firstBin[d] = clampi(trunc_to_int(lo[d]), 0, kNumSpatialBins - 1);
+                    lastBin[d] = clampi(trunc_to_int(hi[d]), firstBin[d], kNumSpatialBins - 1);
                 }
-                bin(dim, lastBin[dim]).bounds.grow(curr.bounds);
-                bin(dim, firstBin[dim]).enter++;
-                bin(dim, lastBin[dim]).exit++;
+                for (int dim = 0; dim < 3; dim++) {
+                    Ref curr = ref;
+                    for (int i = firstBin[dim]; i < lastBin[dim]; i++) {
+                        Ref l, r;
+                        split_reference(l, r, curr, dim, origin[dim] + binSize[dim] * (float)(i + 1));
+                        out[dim * kNumSpatialBins + i].bounds.grow(l.bounds);
+                        out[dim * kNumSpatialBins + i].grown = true;
+                        curr = r;
+                    }
+                    out[dim * kNumSpatialBins + lastBin[dim]].bounds.grow(curr.bounds);
+                    out[dim * kNumSpatialBins + lastBin[dim]].grown = true;
+                    out[dim * kNumSpatialBins + firstBin[dim]].enter++;
+                    out[dim * kNumSpatialBins + lastBin[dim]].exit++;
+                }
             }
+        };
+        std::vector<SpatialBin> bins;
+        const size_t n = refs.size();
+        const int chunks = n >= (size_t)kParallelBinRefs ? kBinThreads : 1;
+        if (chunks == 1) {
+            bin_refs(0, n, bins);
+        } else {
+            std::vector<std::vector<SpatialBin>> part(chunks);
+            std::vector<std::thread> th;
+            for (int c = 1; c < chunks; c++) th.emplace_back(bin_refs, n * c / chunks, n * (c + 1) / chunks, std::ref(part[c]));
+            bin_refs(0, n / chunks, part[0]);
+            for (auto& t : th) t.join();
+            bins = std::move(part[0]);
+            for (int c = 1; c < chunks; c++)
+                for (size_t b = 0; b < bins.size(); b++) {
+                    if (part[c][b].grown) {   // an untouched chunk bin is the empty AABB: growing by it is not a no-op
+                        bins[b].bounds.grow(part[c][b].bounds);
+                        bins[b].grown = true;
+                    }
+                    bins[b].enter += part[c][b].enter;
+                    bins[b].exit += part[c][b].exit;
+                }
         }
+        auto bin = [&](int dim, int i) -> SpatialBin& { return bins[dim * kNumSpatialBins + i]; };
 
         SpatialSplit split;
         AABB rightBounds[kNumSpatialBins - 1];
