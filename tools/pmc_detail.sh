@@ -15,7 +15,7 @@ import csv, glob, collections
 agg = collections.defaultdict(list)
 for f in glob.glob("gpurun_out/pmcd/p*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
-        if "trace_kernel<16, false, true, true, false>" in r["Kernel_Name"]:
+        if "trace_kernel<16, false, true, true, false, false, false>" in r["Kernel_Name"]:
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k in sorted(agg):
     v = agg[k]
