@@ -81,6 +81,39 @@ int mrth_scene_copy_arrays(const mrth_scene* s, float* vertices, int32_t* triang
     return MRTH_OK;
 }
 
+namespace {
+// Vec4f::toABGR, host variant (reference Math.cc:45-52): clamp, scale by 2^56 in
+// double, times 255, round half up in fixed point.
+uint32_t host_to_abgr(const float v[4]) {
+    uint32_t r = 0;
+    for (int i = 0; i < 4; i++) {
+        const float c = v[i] < 0.0f ? 0.0f : (v[i] > 1.0f ? 1.0f : v[i]);
+        const uint64_t q = (uint64_t)((double)c * 72057594037927936.0);   // exp2(56)
+        r |= (uint32_t)((((q * 255u) >> 55) + 1) >> 1) << (8 * i);
+    }
+    return r;
+}
+}  // namespace
+
+int mrth_scene_tri_colors(const mrth_scene* s, uint32_t* material, uint32_t* shaded) {
+    if (!s) return fail(MRTH_ERR_INVALID_ARG, "null scene");
+    // Scene::Scene (reference Scene.cc:37,68-80) with the default material of every
+    // submesh we load (MeshBase::Material, Mesh.hh:92: diffuse (0.75, 0.75, 0.75, 1)).
+    const float diffuse[4] = {0.75f, 0.75f, 0.75f, 1.0f};
+    const mrt::Vec3f light = mrt::normalize(mrt::Vec3f{1.0f, 2.0f, 3.0f});
+    const uint32_t mat = host_to_abgr(diffuse);
+    const size_t nt = s->scene.triNormals.size();
+    for (size_t i = 0; i < nt; i++) {
+        if (material) material[i] = mat;
+        if (shaded) {
+            const float k = mrt::dot(s->scene.triNormals[i], light) * 0.5f + 0.5f;
+            const float c[4] = {diffuse[0] * k, diffuse[1] * k, diffuse[2] * k, 1.0f};
+            shaded[i] = host_to_abgr(c);
+        }
+    }
+    return MRTH_OK;
+}
+
 int mrth_scene_camera(const mrth_scene* s, mrth_camera* cam, float* aoRadius) {
     if (!s || !cam) return fail(MRTH_ERR_INVALID_ARG, "null argument");
     const mrt::Camera& c = s->scene.camera;

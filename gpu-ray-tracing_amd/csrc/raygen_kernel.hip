@@ -6,6 +6,8 @@
 //                          RayGenKernels.cu:79-113)
 //   mrt_raygen_ao       <- RayGen::ao + rayGenAOKernel (RayGen.cc:77-120, RayGenKernels.cu:117-227)
 //   mrt_count_hits      <- countHitsKernel / launch_countHitsKernel (RendererKernels.cu:112-162,189-)
+//   mrt_reconstruct     <- reconstructKernel / launch_reconstructKernel (RendererKernels.cu:60-108,
+//                          Renderer.cc:421-445)
 //
 // The per-ray arithmetic is csrc/raygen_common.hpp, the same code the host
 // generator runs. These are streaming kernels (32 B written per ray, 16-48 B
@@ -105,6 +107,63 @@ __global__ __launch_bounds__(kThreads) void count_final_kernel(const int32_t* pa
     }
 }
 
+struct ReconstructArgs {
+    int numRaysPerPrimary, firstPrimary, numPrimary, rayType;
+    const int32_t* primarySlotToId;
+    const int4* primaryResults;
+    const int32_t* batchIdToSlot;   // NULL: identity (the device/host generators' layout)
+    const int4* batchResults;
+    const uint32_t* triMaterialColor;
+    const uint32_t* triShadedColor;
+    uint32_t* pixels;
+};
+
+// fromABGR / toABGR of RendererKernels.cu:38-56 (device variant: truncating, not rounding).
+__device__ inline float4 from_abgr(uint32_t c) {
+    const float k = 1.0f / 255.0f;
+    return make_float4((float)(c & 0xFF) * k, (float)((c >> 8) & 0xFF) * k, (float)((c >> 16) & 0xFF) * k,
+                       (float)(c >> 24) * k);
+}
+__device__ inline uint32_t to_abgr(float4 v) {
+    return (uint32_t)(fminf(fmaxf(v.x, 0.0f), 1.0f) * 255.0f) |
+           ((uint32_t)(fminf(fmaxf(v.y, 0.0f), 1.0f) * 255.0f) << 8) |
+           ((uint32_t)(fminf(fmaxf(v.z, 0.0f), 1.0f) * 255.0f) << 16) |
+           ((uint32_t)(fminf(fmaxf(v.w, 0.0f), 1.0f) * 255.0f) << 24);
+}
+
+// One thread per primary ray of the batch: average the batch rays' colours
+// (background / white / shaded triangle colour), modulate by the primary hit's
+// material for diffuse, write one ABGR pixel (RendererKernels.cu:60-108).
+// Streaming: 16 B per result read + 4 B colour gathers (L2-resident tables), 4 B written.
+__global__ __launch_bounds__(kThreads) void reconstruct_kernel(ReconstructArgs a) {
+    const int task = (int)(blockIdx.x * kThreads + threadIdx.x);
+    if (task >= a.numPrimary) return;
+    const int n = a.numRaysPerPrimary;
+    const bool isPrimary = a.rayType == MRT_RAY_PRIMARY, isAO = a.rayType == MRT_RAY_AO;
+    const int primarySlot = a.firstPrimary + task;
+    const int primaryId = a.primarySlotToId[primarySlot];
+    const int batchBase = isPrimary ? primaryId : task * n;
+    const float4 bg = make_float4(0.2f, 0.4f, 0.8f, 1.0f);
+    float4 c = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    for (int i = 0; i < n; i++) {
+        const int slot = a.batchIdToSlot ? a.batchIdToSlot[batchBase + i] : (isPrimary ? primarySlot : batchBase + i);
+        const int tri = a.batchResults[slot].x;
+        float4 add;
+        if (tri == -1) add = isPrimary ? bg : make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+        else add = isAO ? make_float4(0.0f, 0.0f, 0.0f, 1.0f) : from_abgr(a.triShadedColor[tri]);
+        c.x += add.x; c.y += add.y; c.z += add.z; c.w += add.w;
+    }
+    const float inv = 1.0f / (float)n;
+    c.x *= inv; c.y *= inv; c.z *= inv; c.w *= inv;
+    const int tri = a.primaryResults[primarySlot].x;
+    if (isAO && tri == -1) c = bg;
+    if (a.rayType == MRT_RAY_DIFFUSE) {
+        const float4 m = tri == -1 ? bg : from_abgr(a.triMaterialColor[tri]);
+        c.x *= m.x; c.y *= m.y; c.z *= m.z; c.w *= m.w;
+    }
+    a.pixels[primaryId] = to_abgr(c);
+}
+
 int hip_fail(hipError_t e, const char* what) {
     return api_fail(MRT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
@@ -191,6 +250,38 @@ int mrt_count_hits(const void* results, int32_t numRays, int32_t* hitCount, void
     const hipError_t f = hipFreeAsync(partial, s);
     if (e != hipSuccess) return hip_fail(e, "count hits launch");
     return f == hipSuccess ? MRT_OK : hip_fail(f, "hipFreeAsync(count partials)");
+}
+
+int mrt_reconstruct(int32_t rayType, int32_t numRaysPerPrimary, int32_t firstPrimary, int32_t numPrimary,
+                    const int32_t* primarySlotToId, const void* primaryResults, const int32_t* batchIdToSlot,
+                    const void* batchResults, const uint32_t* triMaterialColor, const uint32_t* triShadedColor,
+                    uint32_t* pixels, void* stream) {
+    if (rayType < MRT_RAY_PRIMARY || rayType > MRT_RAY_DIFFUSE) return api_fail(MRT_ERR_INVALID_ARG, "bad ray type");
+    if (numRaysPerPrimary < 1 || firstPrimary < 0 || numPrimary < 0 ||
+        (rayType == MRT_RAY_PRIMARY && numRaysPerPrimary != 1))
+        return api_fail(MRT_ERR_INVALID_ARG, "bad batch shape");
+    if ((int64_t)numPrimary * numRaysPerPrimary > INT32_MAX || (int64_t)firstPrimary + numPrimary > INT32_MAX)
+        return api_fail(MRT_ERR_TOO_LARGE, "too many rays");
+    if (numPrimary == 0) return MRT_OK;
+    if (!primarySlotToId || !primaryResults || !batchResults || !pixels ||
+        (rayType != MRT_RAY_AO && !triShadedColor) || (rayType == MRT_RAY_DIFFUSE && !triMaterialColor))
+        return api_fail(MRT_ERR_INVALID_ARG, "null argument");
+    ReconstructArgs a{};
+    a.numRaysPerPrimary = numRaysPerPrimary;
+    a.firstPrimary = firstPrimary;
+    a.numPrimary = numPrimary;
+    a.rayType = rayType;
+    a.primarySlotToId = primarySlotToId;
+    a.primaryResults = static_cast<const int4*>(primaryResults);
+    a.batchIdToSlot = batchIdToSlot;
+    a.batchResults = static_cast<const int4*>(batchResults);
+    a.triMaterialColor = triMaterialColor;
+    a.triShadedColor = triShadedColor;
+    a.pixels = pixels;
+    hipLaunchKernelGGL(reconstruct_kernel, dim3((numPrimary + kThreads - 1) / kThreads), dim3(kThreads), 0,
+                       static_cast<hipStream_t>(stream), a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MRT_OK : hip_fail(e, "reconstruct launch");
 }
 
 }  // extern "C"

@@ -79,6 +79,7 @@ TRACE_SYMBOLS = [
                                           vp]),
     ("mrt_raygen_ao", i32, [vp, vp, i32, vp, i64, i32, f32, u32, vp, vp, vp, vp]),
     ("mrt_count_hits", i32, [vp, i32, vp, vp]),
+    ("mrt_reconstruct", i32, [i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp]),
     ("mrt_selftest_exact_rcp", i32, [C.POINTER(C.c_uint64)]),
     ("bind_CudaBVHTexture", None, [vp, i64, vp, i64, vp, i64]),
     ("unbind_CudaBVHTexture", None, []),
@@ -96,6 +97,7 @@ HOST_SYMBOLS = [
     ("mrth_scene_num_vertices", i64, [vp]),
     ("mrth_scene_copy_arrays", i32, [vp, vp, vp, vp]),
     ("mrth_scene_camera", i32, [vp, C.POINTER(HostCamera), C.POINTER(f32)]),
+    ("mrth_scene_tri_colors", i32, [vp, vp, vp]),
     ("mrth_default_build_params", None, [C.POINTER(BuildParams)]),
     ("mrth_bvh_build", i32, [vp, C.POINTER(BuildParams), C.POINTER(vp)]),
     ("mrth_bvh_load", i32, [C.c_char_p, C.POINTER(vp)]),

@@ -96,6 +96,14 @@ class Scene:
         _lib.check_host(_lib.host_lib().mrth_scene_copy_arrays(self._h, _ptr(v), _ptr(t), _ptr(n)))
         return v, t, n
 
+    def tri_colors(self):
+        """(material, shaded) ABGR uint32 per triangle (Scene::Scene, reference Scene.cc:47-80)."""
+        nt = self.num_triangles
+        mat = np.empty(nt, np.uint32)
+        sh = np.empty(nt, np.uint32)
+        _lib.check_host(_lib.host_lib().mrth_scene_tri_colors(self._h, _ptr(mat), _ptr(sh)))
+        return mat, sh
+
     def camera(self):
         c = _lib.HostCamera()
         ao = C.c_float()
@@ -204,3 +212,16 @@ def ao_rays(primary: np.ndarray, primary_results: np.ndarray, scene: Scene, max_
 def count_hits(results: np.ndarray) -> int:
     r = np.ascontiguousarray(results).view(np.int32).reshape(-1, 4)
     return int(_lib.host_lib().mrth_count_hits(_ptr(r), len(r)))
+
+
+def write_ppm(path: str, pixels: np.ndarray, w: int, h: int, flip: bool = True) -> None:
+    """Binary PPM (P6) of w*h ABGR uint32 pixels indexed y*w + x (the reference's
+    PBO, Renderer.cc:221-238). flip=True writes row h-1 first: the reference drew
+    the PBO with GL, whose row 0 is the bottom of the window."""
+    px = np.ascontiguousarray(pixels, np.uint32).reshape(h, w)
+    if flip:
+        px = px[::-1]
+    rgb = np.stack([px & 0xFF, (px >> 8) & 0xFF, (px >> 16) & 0xFF], axis=-1).astype(np.uint8)
+    with open(path, "wb") as f:
+        f.write(b"P6\n%d %d\n255\n" % (w, h))
+        f.write(rgb.tobytes())

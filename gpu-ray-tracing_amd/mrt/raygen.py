@@ -80,3 +80,41 @@ class DeviceRayGen:
 
     def count_hits(self, rays: RayBuffer, stream=None) -> int:
         return int(self.count_hits_async(rays, stream).item())
+
+
+RAY_PRIMARY, RAY_AO, RAY_DIFFUSE = 0, 1, 2
+
+
+class DeviceReconstructor:
+    """Renderer's reconstruction step on one device (reference Renderer.cc:421-445 +
+    reconstructKernel, RendererKernels.cu:60-108): traced batches -> ABGR pixels in HBM."""
+
+    def __init__(self, scene: Scene, device=None):
+        self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.lib = _lib.trace_lib()
+        mat, sh = scene.tri_colors()
+        self.material = torch.from_numpy(mat.view(np.int32)).to(self.device)
+        self.shaded = torch.from_numpy(sh.view(np.int32)).to(self.device)
+
+    def reconstruct(self, ray_type: int, primary: RayBuffer, slot_to_id: torch.Tensor, num_pixels: int,
+                    batch: RayBuffer | None = None, num_samples: int = 1, pixels: torch.Tensor | None = None,
+                    batch_id_to_slot: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+        """num_pixels int32 (ABGR bits) pixels; batch defaults to the primary batch.
+        AO/diffuse batches hold num_samples rays per primary ray (mrt_raygen_ao's layout)."""
+        if batch is None:
+            batch = primary
+        n_primary = primary.size
+        if ray_type == RAY_PRIMARY and (num_samples != 1 or batch.size != n_primary):
+            raise _lib.MrtError("primary reconstruction takes the primary batch with one ray per pixel")
+        if ray_type != RAY_PRIMARY and batch.size != n_primary * num_samples:
+            raise _lib.MrtError(f"batch holds {batch.size} rays, expected {n_primary} x {num_samples}")
+        if slot_to_id.numel() != n_primary:
+            raise _lib.MrtError("slot_to_id must hold one pixel id per primary ray")
+        if pixels is None:
+            pixels = torch.zeros(num_pixels, dtype=torch.int32, device=self.device)
+        b2s = None if batch_id_to_slot is None else batch_id_to_slot.data_ptr()
+        _lib.check(self.lib.mrt_reconstruct(ray_type, num_samples, 0, n_primary, slot_to_id.data_ptr(),
+                                            primary.results.data_ptr(), b2s, batch.results.data_ptr(),
+                                            self.material.data_ptr(), self.shaded.data_ptr(), pixels.data_ptr(),
+                                            _stream_ptr(stream)))
+        return pixels

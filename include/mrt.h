@@ -161,6 +161,25 @@ int  mrt_raygen_ao(const void* inRays, const void* inResults, int32_t numInputRa
  * results with id >= 0. */
 int  mrt_count_hits(const void* results, int32_t numRays, int32_t* hitCount, void* stream);
 
+/* ray types of a batch (reference RayType_Primary / _AO / _Diffuse, App.cc) */
+enum { MRT_RAY_PRIMARY = 0, MRT_RAY_AO = 1, MRT_RAY_DIFFUSE = 2 };
+
+/* reconstructKernel (RendererKernels.cu:60-108; ReconstructInput RendererKernels.hh:46-61,
+ * filled by Renderer.cc:421-445): one ABGR pixel per primary ray of the batch, at
+ * pixels[primarySlotToId[firstPrimary + i]], i < numPrimary. Primary: shaded colour of
+ * the hit triangle or the background (0.2, 0.4, 0.8); AO: the fraction of unblocked
+ * rays (background where the primary missed); diffuse: the average shaded colour of
+ * the bounce hits (white for misses) times the primary hit's material colour. Batch
+ * rays of primary task i are batchIdToSlot[i * numRaysPerPrimary + k] (primary:
+ * batchIdToSlot[pixel id]); batchIdToSlot NULL = identity layout (mrt_raygen_ao's).
+ * Results are RayResult (16 B); colour tables one ABGR uint32 per triangle
+ * (mrth_scene_tri_colors). Colour arithmetic is the reference's device code: float
+ * sums in ray order, truncating toABGR. */
+int  mrt_reconstruct(int32_t rayType, int32_t numRaysPerPrimary, int32_t firstPrimary, int32_t numPrimary,
+                     const int32_t* primarySlotToId, const void* primaryResults, const int32_t* batchIdToSlot,
+                     const void* batchResults, const uint32_t* triMaterialColor, const uint32_t* triShadedColor,
+                     uint32_t* pixels, void* stream);
+
 /* ---- per-device convenience API (one implicit tracer per device) -------- */
 int  mrt_bind_bvh(const void* nodes, int64_t nodeBytes, const void* woop, int64_t woopBytes,
                   const int32_t* triIndex, int64_t triIndexBytes);

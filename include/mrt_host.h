@@ -63,6 +63,12 @@ int64_t mrth_scene_num_vertices(const mrth_scene* s);
 int  mrth_scene_copy_arrays(const mrth_scene* s, float* vertices /* 3*nv or NULL */,
                             int32_t* triangles /* 3*nt or NULL */, float* normals /* 3*nt or NULL */);
 int  mrth_scene_camera(const mrth_scene* s, mrth_camera* cam, float* aoRadius);
+/* Per-triangle ABGR colour tables of Scene::Scene (reference Scene.cc:47-80): the
+ * material colour and the shaded colour diffuse * (dot(n, normalize(1,2,3)) / 2 + 1/2),
+ * both through the host Vec4f::toABGR (Math.cc:45-52). Every triangle carries the default
+ * material (diffuse 0.75 grey, Mesh.hh:92): the loaders keep no .mtl colours. Either
+ * output may be NULL; each holds num_triangles uint32. */
+int  mrth_scene_tri_colors(const mrth_scene* s, uint32_t* material, uint32_t* shaded);
 
 /* ---- BVH (SBVH build -> Compact2 host buffers) ---------------------------- */
 void mrth_default_build_params(mrth_build_params* p);

@@ -29,6 +29,10 @@ def lib():
         L.oracle_woop_hit.argtypes = [vp, vp, i64, i64, C.c_float, C.POINTER(C.c_float)]
         L.oracle_brute_force.restype = None
         L.oracle_brute_force.argtypes = [vp, vp, i64, C.c_int, vp, i64, vp]
+        L.oracle_tri_colors.restype = None
+        L.oracle_tri_colors.argtypes = [vp, i64, vp, vp]
+        L.oracle_reconstruct.restype = None
+        L.oracle_reconstruct.argtypes = [C.c_int] * 4 + [vp] * 7
         _lib = L
     return _lib
 
@@ -66,3 +70,30 @@ def brute_force(rays, woop, tri_index, any_hit=False):
     res = np.zeros((len(rays), 4), np.int32)
     lib().oracle_brute_force(_p(rays), _p(res), len(rays), int(any_hit), _p(woop), woop.nbytes, _p(tri))
     return res
+
+
+def tri_colors(normals):
+    """Scene::Scene colour tables (material, shaded) as uint32 ABGR."""
+    normals = np.ascontiguousarray(normals, np.float32).reshape(-1, 3)
+    n = normals.shape[0]
+    mat = np.empty(n, np.uint32)
+    sh = np.empty(n, np.uint32)
+    lib().oracle_tri_colors(_p(normals), n, _p(mat), _p(sh))
+    return mat, sh
+
+
+def reconstruct(ray_type, num_rays_per_primary, primary_slot_to_id, primary_results, batch_results,
+                tri_material, tri_shaded, num_pixels, batch_id_to_slot=None, first_primary=0, num_primary=None):
+    """reconstructKernel on the CPU; returns num_pixels uint32 ABGR (untouched pixels 0)."""
+    s2i = np.ascontiguousarray(primary_slot_to_id, np.int32)
+    pres = np.ascontiguousarray(primary_results, np.int32).reshape(-1, 4)
+    bres = np.ascontiguousarray(batch_results, np.int32).reshape(-1, 4)
+    mat = np.ascontiguousarray(tri_material, np.uint32)
+    sh = np.ascontiguousarray(tri_shaded, np.uint32)
+    if num_primary is None:
+        num_primary = s2i.shape[0] - first_primary
+    b2s = None if batch_id_to_slot is None else np.ascontiguousarray(batch_id_to_slot, np.int32)
+    pix = np.zeros(num_pixels, np.uint32)
+    lib().oracle_reconstruct(ray_type, num_rays_per_primary, first_primary, num_primary, _p(s2i), _p(pres),
+                             None if b2s is None else _p(b2s), _p(bres), _p(mat), _p(sh), _p(pix))
+    return pix

@@ -1,0 +1,168 @@
+"""Frame reconstruction — the consumer of the traced batches (reference
+reconstructKernel, src/rt/cuda/RendererKernels.cu:60-108, fed by
+Renderer.cc:421-445, with Scene::Scene's colour tables, Scene.cc:47-80).
+
+CPU tests pin the oracle (tests/oracle_lib.py -> oracle/trace_oracle.c) with
+hand-computed answers and check the host colour tables against it; GPU tests
+compare mrt_reconstruct bit for bit with the oracle on traced frames. Parity
+unpinned against executed reference output (none exists)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import mrt
+import oracle_lib as O
+
+BG = 0xFFCC6633          # toABGR(0.2, 0.4, 0.8, 1) with the device's truncation: 51, 102, 204, 255
+GREY = 0xFFBFBFBF        # 0.75 * 255 = 191.25 -> 191 (host rounds, device truncates: both 191)
+
+
+def res(ids):
+    r = np.zeros((len(ids), 4), np.int32)
+    r[:, 0] = ids
+    return r
+
+
+# ---------------------------------------------------------------- CPU: the oracle
+def test_tri_colors_known_answers():
+    light = np.array([1, 2, 3], np.float32) / np.float32(np.sqrt(np.float32(14)))
+    normals = np.stack([light, -light, np.zeros(3, np.float32)])
+    mat, sh = O.tri_colors(normals)
+    assert (mat == GREY).all()                       # diffuse 0.75 grey, alpha 1
+    assert sh[0] == GREY                             # facing the light: k = 1
+    assert sh[1] == 0xFF000000                       # facing away: k = 0
+    assert sh[2] == 0xFF606060                       # k = 1/2: 0.375 * 255 = 95.625 rounds to 96
+
+
+def test_host_tri_colors_equal_the_oracle():
+    scene = mrt.Scene.synthetic("conference", 0, 1)
+    _, _, normals = scene.arrays()
+    mat, sh = scene.tri_colors()
+    omat, osh = O.tri_colors(normals)
+    assert np.array_equal(mat, omat) and np.array_equal(sh, osh)
+    assert len(np.unique(sh)) > 20                   # shading varies with the normal
+
+
+def test_reconstruct_primary_known_answers():
+    # two pixels traced in swapped order: slot 0 -> pixel 1 (hit tri 1), slot 1 -> pixel 0 (miss)
+    shaded = np.array([0, 0xFF00FF00], np.uint32)
+    p = res([1, -1])
+    pix = O.reconstruct(0, 1, [1, 0], p, p, shaded, shaded, 2)
+    assert pix.tolist() == [BG, 0xFF00FF00]
+
+
+def test_reconstruct_ao_known_answers():
+    prim = res([5, -1])
+    # primary 0 (hit): 3 of 4 samples unblocked -> (0.75, 0.75, 0.75, 1); primary 1 missed -> background
+    batch = res([-1, 7, -1, -1, -1, -1, -1, -1])
+    pix = O.reconstruct(1, 4, [0, 1], prim, batch, np.zeros(8, np.uint32), np.zeros(8, np.uint32), 2)
+    assert pix.tolist() == [GREY, BG]
+    # every sample blocked -> black with alpha 1
+    pix = O.reconstruct(1, 4, [0, 1], prim, res([3] * 8), np.zeros(8, np.uint32), np.zeros(8, np.uint32), 2)
+    assert pix[0] == 0xFF000000
+
+
+def test_reconstruct_diffuse_known_answers():
+    material = np.array([0xFF0000FF, 0], np.uint32)  # tri 0: red
+    shaded = np.array([0, 0xFFFFFFFF], np.uint32)    # tri 1 shades white
+    prim = res([0, -1])
+    batch = res([-1, 1, -1, -1])                      # two bounces each: miss (white) + white, miss + miss
+    pix = O.reconstruct(2, 2, [0, 1], prim, batch, material, shaded, 2)
+    assert pix[0] == 0xFF0000FF                       # white * red
+    assert pix[1] == BG                               # white * background
+
+
+def test_reconstruct_honours_slot_maps_and_batch_window():
+    prim = res([-1, -1, -1])
+    batch = res([2, -1])                              # one AO sample per primary ray of the window
+    shaded = np.zeros(3, np.uint32)
+    # window = primaries 1..2 of the frame (firstPrimary 1): batch task i -> batch slot b2s[i]
+    pix = O.reconstruct(1, 1, [2, 0, 1], res([-1, 4, 4]), batch, shaded, shaded, 3, batch_id_to_slot=[1, 0],
+                        first_primary=1, num_primary=2)
+    assert pix.tolist() == [0xFFFFFFFF, 0xFF000000, 0]
+    del prim
+
+
+def test_write_ppm(tmp_path):
+    px = np.array([0xFF0000FF, 0xFF00FF00, 0xFFFF0000, 0xFFFFFFFF], np.uint32)   # ABGR: red, green, blue, white
+    path = os.path.join(tmp_path, "f.ppm")
+    mrt.write_ppm(path, px, 2, 2, flip=False)
+    data = open(path, "rb").read()
+    assert data.startswith(b"P6\n2 2\n255\n")
+    assert data[-12:] == bytes([255, 0, 0, 0, 255, 0, 0, 0, 255, 255, 255, 255])
+    mrt.write_ppm(path, px, 2, 2)                    # flipped: bottom row first
+    assert open(path, "rb").read()[-12:] == bytes([0, 0, 255, 255, 255, 255, 255, 0, 0, 0, 255, 0])
+
+
+# ---------------------------------------------------------------- GPU: mrt_reconstruct
+@pytest.fixture(scope="module")
+def frame():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mrt.raygen import DeviceRayGen, DeviceReconstructor
+    from mrt.tracer import GpuBvh, Tracer
+    scene = mrt.Scene.synthetic("sponza", 0, 1)
+    cam, ao = scene.camera()
+    bufs = mrt.Bvh.build(scene).buffers()
+    t = Tracer(0)
+    t.set_bvh(GpuBvh(bufs))
+    return scene, cam, ao, bufs, t, DeviceRayGen(scene), DeviceReconstructor(scene)
+
+
+def _oracle_pixels(scene, ray_type, n, s2i, pres, bres, w, h):
+    mat, sh = O.tri_colors(scene.arrays()[2])
+    return O.reconstruct(ray_type, n, s2i, pres, bres, mat, sh, w * h)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ray_type,samples", [(0, 1), (1, 1), (1, 8), (2, 1), (2, 4)])
+def test_device_reconstruct_equals_the_oracle(frame, ray_type, samples):
+    scene, cam, ao, bufs, t, g, rec = frame
+    w, h = 160, 96
+    prim, s2i = g.primary(cam, w, h)
+    t.trace_batch(prim, exact_rcp=True)
+    batch = None
+    if ray_type == 1:
+        batch = g.ao(prim, samples, ao)
+    elif ray_type == 2:
+        batch = g.ao(prim, samples, cam.far, closest_hit=True)
+    if batch is not None:
+        t.trace_batch(batch, exact_rcp=True)
+    pix = rec.reconstruct(ray_type, prim, s2i, w * h, batch=batch, num_samples=samples)
+    dev = pix.cpu().numpy().view(np.uint32)
+    bres = (batch if batch is not None else prim).results_numpy()
+    want = _oracle_pixels(scene, ray_type, samples, s2i.cpu().numpy(), prim.results_numpy(), bres, w, h)
+    assert np.array_equal(dev, want)
+    # a real image, not a constant (AO: background, black, white and the partial levels)
+    assert len(np.unique(dev)) >= (3 if ray_type == 1 else 9)
+
+
+@pytest.mark.gpu
+def test_device_primary_frame_end_to_end(frame, tmp_path):
+    """Device raygen -> trace -> reconstruct against host rays -> oracle trace -> oracle reconstruct."""
+    scene, cam, ao, bufs, t, g, rec = frame
+    w, h = 200, 150
+    prim, s2i = g.primary(cam, w, h)
+    t.trace_batch(prim)                              # production mode: closest hit bit-identical
+    dev = rec.reconstruct(0, prim, s2i, w * h).cpu().numpy().view(np.uint32)
+    host_rays, host_s2i = mrt.primary_rays(cam, w, h)
+    hres, _, _ = O.trace(host_rays, *bufs, threads=8)
+    assert np.array_equal(dev, _oracle_pixels(scene, 0, 1, host_s2i, hres, hres, w, h))
+    mrt.write_ppm(os.path.join(tmp_path, "sponza.ppm"), dev, w, h)
+
+
+@pytest.mark.gpu
+def test_device_reconstruct_rejects_bad_shapes(frame):
+    scene, cam, ao, bufs, t, g, rec = frame
+    prim, s2i = g.primary(cam, 8, 8)
+    with pytest.raises(mrt._lib.MrtError):
+        rec.reconstruct(1, prim, s2i, 64, batch=prim, num_samples=4)
+
+
+def test_reconstruct_argument_checks_without_gpu():
+    lib = mrt._lib.trace_lib()
+    assert lib.mrt_reconstruct(3, 1, 0, 1, 1, 1, None, 1, 1, 1, 1, None) == 1     # bad ray type
+    assert lib.mrt_reconstruct(0, 2, 0, 1, 1, 1, None, 1, 1, 1, 1, None) == 1     # primary takes one ray
+    assert lib.mrt_reconstruct(1, 1, 0, 0, None, None, None, None, None, None, None, None) == 0   # empty
