@@ -516,4 +516,31 @@ void copy_tracing_results(void* result_host, void* result_dev, int32_t size) {
     if (e != hipSuccess) compat_check(hipFail(e, "hipMemcpy"), __FILE__, __LINE__);
 }
 
+void launch_reconstructKernel(int32_t nthreads, mrt_reconstruct_input* in) {
+    (void)nthreads;   // the reference's CudaKernel::setGrid(nthreads) shape; ours is fixed
+    if (!in) compat_check(fail(MRT_ERR_INVALID_ARG, "null ReconstructInput"), __FILE__, __LINE__);
+    const int32_t type = in->isAO ? MRT_RAY_AO : (in->isDiffuse ? MRT_RAY_DIFFUSE : MRT_RAY_PRIMARY);
+    compat_check(mrt_reconstruct(type, in->numRaysPerPrimary, in->firstPrimary, in->numPrimary, in->primarySlotToID,
+                                 in->primaryResults, in->batchIDToSlot, in->batchResults, in->triMaterialColor,
+                                 in->triShadedColor, in->pixels, nullptr),
+                 __FILE__, __LINE__);
+    const hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) compat_check(hipFail(e, "hipDeviceSynchronize"), __FILE__, __LINE__);
+}
+
+int32_t launch_countHitsKernel(int32_t threads, const int32_t* blockSize, mrt_count_hits_input* in) {
+    (void)threads; (void)blockSize;   // launch shape of the reference (RendererKernels.cu:191-199)
+    if (!in) compat_check(fail(MRT_ERR_INVALID_ARG, "null CountHitsInput"), __FILE__, __LINE__);
+    int32_t* d = nullptr;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&d), sizeof(int32_t));
+    if (e != hipSuccess) compat_check(hipFail(e, "hipMalloc"), __FILE__, __LINE__);
+    compat_check(mrt_count_hits(in->rayResults, in->numRays, d, nullptr), __FILE__, __LINE__);
+    int32_t n = 0;
+    e = hipMemcpy(&n, d, sizeof(int32_t), hipMemcpyDeviceToHost);
+    const hipError_t f = hipFree(d);
+    if (e != hipSuccess) compat_check(hipFail(e, "hipMemcpy"), __FILE__, __LINE__);
+    if (f != hipSuccess) compat_check(hipFail(f, "hipFree"), __FILE__, __LINE__);
+    return n;
+}
+
 }  // extern "C"

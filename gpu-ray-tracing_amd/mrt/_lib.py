@@ -85,6 +85,8 @@ TRACE_SYMBOLS = [
     ("unbind_CudaBVHTexture", None, []),
     ("launch_tracingKernel", f32, [i32, vp, C.c_int, C.c_bool, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     ("copy_tracing_results", None, [vp, vp, i32]),
+    ("launch_reconstructKernel", None, [i32, vp]),
+    ("launch_countHitsKernel", i32, [i32, vp, vp]),
 ]
 
 # (name, restype, argtypes) of every symbol include/mrt_host.h declares.

@@ -206,6 +206,33 @@ float launch_tracingKernel(int32_t nthreads, int32_t* blockSize, int numRays, bo
                            void* trisA, void* trisB, void* trisC, int32_t* triIndices);
 void  copy_tracing_results(void* result_host, void* result_dev, int32_t size);
 
+/* RendererKernels.hh:46-69 input structs, field for field (same C layout: three int32,
+ * three bools, then 8-byte-aligned pointers). The reference passes them by C++
+ * reference, which is ABI-identical to a pointer. Both launchers synchronise like
+ * the reference's (cudaDeviceSynchronize) and ignore its launch-shape arguments. */
+typedef struct mrt_reconstruct_input {
+    int32_t   numRaysPerPrimary, firstPrimary, numPrimary;
+    bool      isPrimary, isAO, isDiffuse;
+    int32_t*  primarySlotToID;
+    void*     primaryResults;
+    int32_t*  batchIDToSlot;
+    void*     batchResults;
+    uint32_t* triMaterialColor;
+    uint32_t* triShadedColor;
+    uint32_t* pixels;
+} mrt_reconstruct_input;
+
+typedef struct mrt_count_hits_input {
+    int32_t numRays;
+    void*   rayResults;
+    int32_t raysPerThread;
+} mrt_count_hits_input;
+
+/* launch_reconstructKernel (RendererKernels.cu:166-186) */
+void    launch_reconstructKernel(int32_t nthreads, mrt_reconstruct_input* in);
+/* launch_countHitsKernel (RendererKernels.cu:189-215): returns the hit count */
+int32_t launch_countHitsKernel(int32_t threads, const int32_t* blockSize, mrt_count_hits_input* in);
+
 #ifdef __cplusplus
 }
 #endif

@@ -6,6 +6,7 @@ CPU tests pin the oracle (tests/oracle_lib.py -> oracle/trace_oracle.c) with
 hand-computed answers and check the host colour tables against it; GPU tests
 compare mrt_reconstruct bit for bit with the oracle on traced frames. Parity
 unpinned against executed reference output (none exists)."""
+import ctypes as C
 import os
 
 import numpy as np
@@ -166,3 +167,45 @@ def test_reconstruct_argument_checks_without_gpu():
     assert lib.mrt_reconstruct(3, 1, 0, 1, 1, 1, None, 1, 1, 1, 1, None) == 1     # bad ray type
     assert lib.mrt_reconstruct(0, 2, 0, 1, 1, 1, None, 1, 1, 1, 1, None) == 1     # primary takes one ray
     assert lib.mrt_reconstruct(1, 1, 0, 0, None, None, None, None, None, None, None, None) == 0   # empty
+
+
+class ReconstructInput(C.Structure):
+    """RendererKernels.hh:46-61, field for field (mrt.h mrt_reconstruct_input)."""
+    _fields_ = [("numRaysPerPrimary", C.c_int32), ("firstPrimary", C.c_int32), ("numPrimary", C.c_int32),
+                ("isPrimary", C.c_bool), ("isAO", C.c_bool), ("isDiffuse", C.c_bool),
+                ("primarySlotToID", C.c_void_p), ("primaryResults", C.c_void_p), ("batchIDToSlot", C.c_void_p),
+                ("batchResults", C.c_void_p), ("triMaterialColor", C.c_void_p), ("triShadedColor", C.c_void_p),
+                ("pixels", C.c_void_p)]
+
+
+class CountHitsInput(C.Structure):
+    """RendererKernels.hh:65-70 (mrt.h mrt_count_hits_input)."""
+    _fields_ = [("numRays", C.c_int32), ("rayResults", C.c_void_p), ("raysPerThread", C.c_int32)]
+
+
+def test_compat_input_struct_layout():
+    assert ReconstructInput.primarySlotToID.offset == 16 and C.sizeof(ReconstructInput) == 72
+    assert CountHitsInput.rayResults.offset == 8 and C.sizeof(CountHitsInput) == 24
+
+
+@pytest.mark.gpu
+def test_reference_compat_launchers(frame):
+    """launch_reconstructKernel / launch_countHitsKernel called the way Renderer.cc:421-445 does."""
+    scene, cam, ao, bufs, t, g, rec = frame
+    w, h, n = 96, 64, 4
+    prim, s2i = g.primary(cam, w, h)
+    t.trace_batch(prim)
+    batch = g.ao(prim, n, ao)
+    t.trace_batch(batch)
+    want = rec.reconstruct(1, prim, s2i, w * h, batch=batch, num_samples=n).cpu().numpy()
+    ident = torch.arange(batch.size, dtype=torch.int32, device=prim.results.device)
+    pixels = torch.zeros(w * h, dtype=torch.int32, device=prim.results.device)
+    inp = ReconstructInput(n, 0, prim.size, False, True, False, s2i.data_ptr(), prim.results.data_ptr(),
+                           ident.data_ptr(), batch.results.data_ptr(), rec.material.data_ptr(),
+                           rec.shaded.data_ptr(), pixels.data_ptr())
+    lib = mrt._lib.trace_lib()
+    lib.launch_reconstructKernel(prim.size, C.byref(inp))
+    assert np.array_equal(pixels.cpu().numpy(), want)
+    blk = (C.c_int32 * 2)(32, 8)
+    cnt = CountHitsInput(batch.size, batch.results.data_ptr(), 16)
+    assert lib.launch_countHitsKernel(batch.size, blk, C.byref(cnt)) == g.count_hits(batch)
