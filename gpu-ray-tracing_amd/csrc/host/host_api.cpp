@@ -97,14 +97,15 @@ uint32_t host_to_abgr(const float v[4]) {
 
 int mrth_scene_tri_colors(const mrth_scene* s, uint32_t* material, uint32_t* shaded) {
     if (!s) return fail(MRTH_ERR_INVALID_ARG, "null scene");
-    // Scene::Scene (reference Scene.cc:37,68-80) with the default material of every
-    // submesh we load (MeshBase::Material, Mesh.hh:92: diffuse (0.75, 0.75, 0.75, 1)).
-    const float diffuse[4] = {0.75f, 0.75f, 0.75f, 1.0f};
+    // Scene::Scene (reference Scene.cc:37,68-80): each triangle's submesh material
+    // (OBJ .mtl Kd/d), or the default MeshBase::Material (Mesh.hh:92: diffuse (0.75, 0.75, 0.75, 1)).
+    static const float kDefault[4] = {0.75f, 0.75f, 0.75f, 1.0f};
     const mrt::Vec3f light = mrt::normalize(mrt::Vec3f{1.0f, 2.0f, 3.0f});
-    const uint32_t mat = host_to_abgr(diffuse);
     const size_t nt = s->scene.triNormals.size();
+    const bool perTri = s->scene.triDiffuse.size() == 4 * nt;
     for (size_t i = 0; i < nt; i++) {
-        if (material) material[i] = mat;
+        const float* diffuse = perTri ? &s->scene.triDiffuse[4 * i] : kDefault;
+        if (material) material[i] = host_to_abgr(diffuse);
         if (shaded) {
             const float k = mrt::dot(s->scene.triNormals[i], light) * 0.5f + 0.5f;
             const float c[4] = {diffuse[0] * k, diffuse[1] * k, diffuse[2] * k, 1.0f};

@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <array>
 #include <map>
 #include <sstream>
 #include <string>
@@ -33,6 +34,33 @@ bool parse_index(const char*& p, int count, int* out) {
     return true;
 }
 
+// loadMtl (reference MeshWavefrontIO.cc:114-200): "newmtl" opens a material
+// (diffuse defaults to (0.75, 0.75, 0.75, 1), Mesh.hh:92), "Kd r g b" sets its
+// diffuse rgb, "d a" its alpha; the rest (Ka, Ks, Ns, maps) does not reach the
+// colour tables and is skipped.
+void load_mtl(const std::string& path, std::map<std::string, std::array<float, 4>>& mats) {
+    std::ifstream in(path);
+    if (!in) return;   // the reference ignores a missing library too
+    std::array<float, 4>* cur = nullptr;
+    std::string line;
+    while (std::getline(in, line)) {
+        const char* p = line.c_str();
+        while (*p == ' ' || *p == '\t') ++p;
+        if (std::strncmp(p, "newmtl ", 7) == 0) {
+            std::string name = p + 7;
+            name.erase(0, name.find_first_not_of(" \t"));
+            while (!name.empty() && (name.back() == '\r' || name.back() == ' ')) name.pop_back();
+            cur = &mats.emplace(name, std::array<float, 4>{0.75f, 0.75f, 0.75f, 1.0f}).first->second;
+        } else if (cur && std::strncmp(p, "Kd ", 3) == 0) {
+            float r, g, b;
+            if (std::sscanf(p + 3, "%f %f %f", &r, &g, &b) == 3) { (*cur)[0] = r; (*cur)[1] = g; (*cur)[2] = b; }
+        } else if (cur && std::strncmp(p, "d ", 2) == 0) {
+            float a;
+            if (std::sscanf(p + 2, "%f", &a) == 1) (*cur)[3] = a;
+        }
+    }
+}
+
 }  // namespace
 
 bool load_obj(const std::string& path, Scene& out, std::string* err) {
@@ -45,6 +73,9 @@ bool load_obj(const std::string& path, Scene& out, std::string* err) {
     out.name = path;
     std::vector<std::vector<Vec3i>> submeshes;
     std::map<std::string, int> materialSubmesh;
+    std::map<std::string, std::array<float, 4>> materials;
+    const size_t slash = path.find_last_of('/');
+    const std::string dir = slash == std::string::npos ? std::string(".") : path.substr(0, slash);
     int current = -1, defaultSubmesh = -1;
     int texCount = 0, normalCount = 0;
     std::string line;
@@ -85,6 +116,11 @@ bool load_obj(const std::string& path, Scene& out, std::string* err) {
                 current = defaultSubmesh;
             }
             for (size_t i = 2; i < poly.size(); i++) submeshes[current].push_back(Vec3i{poly[0], poly[i - 1], poly[i]});
+        } else if (std::strncmp(p, "mtllib ", 7) == 0) {
+            std::string name = p + 7;
+            name.erase(0, name.find_first_not_of(" \t"));
+            while (!name.empty() && (name.back() == '\r' || name.back() == ' ')) name.pop_back();
+            if (!name.empty()) load_mtl(dir + "/" + name, materials);
         } else if (std::strncmp(p, "usemtl", 6) == 0) {
             std::string name = p + 6;
             name.erase(0, name.find_first_not_of(" \t"));
@@ -101,7 +137,18 @@ bool load_obj(const std::string& path, Scene& out, std::string* err) {
         if (err) *err = path + ":" + std::to_string(lineNo) + ": malformed line";
         return false;
     }
-    for (const auto& sm : submeshes) out.triangles.insert(out.triangles.end(), sm.begin(), sm.end());
+    std::vector<std::array<float, 4>> smDiffuse(submeshes.size(), std::array<float, 4>{0.75f, 0.75f, 0.75f, 1.0f});
+    bool anyMaterial = false;
+    for (const auto& kv : materialSubmesh) {
+        auto m = materials.find(kv.first);
+        if (m != materials.end()) { smDiffuse[kv.second] = m->second; anyMaterial = true; }
+    }
+    for (size_t i = 0; i < submeshes.size(); i++) {
+        out.triangles.insert(out.triangles.end(), submeshes[i].begin(), submeshes[i].end());
+        if (anyMaterial)
+            for (size_t k = 0; k < submeshes[i].size(); k++)
+                out.triDiffuse.insert(out.triDiffuse.end(), smDiffuse[i].begin(), smDiffuse[i].end());
+    }
     out.compute_normals();
     const AABB b = out.bounds();
     const Vec3f c = (b.mn + b.mx) * 0.5f;

@@ -29,6 +29,7 @@ struct Scene {
     std::vector<Vec3f> vertices;      // getVtxPosBuffer
     std::vector<Vec3i> triangles;     // getTriVtxIndexBuffer
     std::vector<Vec3f> triNormals;    // getTriNormalBuffer (unit face normals)
+    std::vector<float> triDiffuse;    // 4 per triangle: its submesh's Material::diffuse (empty = default 0.75 grey)
     Camera camera;                    // a framing camera for the benchmark
     float aoRadius = 5.0f;            // --ao-radius used with this scene
 

@@ -65,9 +65,10 @@ int  mrth_scene_copy_arrays(const mrth_scene* s, float* vertices /* 3*nv or NULL
 int  mrth_scene_camera(const mrth_scene* s, mrth_camera* cam, float* aoRadius);
 /* Per-triangle ABGR colour tables of Scene::Scene (reference Scene.cc:47-80): the
  * material colour and the shaded colour diffuse * (dot(n, normalize(1,2,3)) / 2 + 1/2),
- * both through the host Vec4f::toABGR (Math.cc:45-52). Every triangle carries the default
- * material (diffuse 0.75 grey, Mesh.hh:92): the loaders keep no .mtl colours. Either
- * output may be NULL; each holds num_triangles uint32. */
+ * both through the host Vec4f::toABGR (Math.cc:45-52). A triangle's material is its OBJ
+ * submesh's .mtl entry (Kd rgb, d alpha; MeshWavefrontIO.cc:114-200) or the default
+ * (diffuse 0.75 grey, Mesh.hh:92; synthetic scenes). Either output may be NULL; each
+ * holds num_triangles uint32. */
 int  mrth_scene_tri_colors(const mrth_scene* s, uint32_t* material, uint32_t* shaded);
 
 /* ---- BVH (SBVH build -> Compact2 host buffers) ---------------------------- */

@@ -31,6 +31,8 @@ def lib():
         L.oracle_brute_force.argtypes = [vp, vp, i64, C.c_int, vp, i64, vp]
         L.oracle_tri_colors.restype = None
         L.oracle_tri_colors.argtypes = [vp, i64, vp, vp]
+        L.oracle_tri_colors_mat.restype = None
+        L.oracle_tri_colors_mat.argtypes = [vp, vp, i64, vp, vp]
         L.oracle_reconstruct.restype = None
         L.oracle_reconstruct.argtypes = [C.c_int] * 4 + [vp] * 7
         _lib = L
@@ -72,13 +74,18 @@ def brute_force(rays, woop, tri_index, any_hit=False):
     return res
 
 
-def tri_colors(normals):
-    """Scene::Scene colour tables (material, shaded) as uint32 ABGR."""
+def tri_colors(normals, diffuse=None):
+    """Scene::Scene colour tables (material, shaded) as uint32 ABGR; diffuse: (n, 4)
+    per-triangle Material::diffuse, None = the default 0.75 grey."""
     normals = np.ascontiguousarray(normals, np.float32).reshape(-1, 3)
     n = normals.shape[0]
     mat = np.empty(n, np.uint32)
     sh = np.empty(n, np.uint32)
-    lib().oracle_tri_colors(_p(normals), n, _p(mat), _p(sh))
+    if diffuse is None:
+        lib().oracle_tri_colors(_p(normals), n, _p(mat), _p(sh))
+    else:
+        d = np.ascontiguousarray(diffuse, np.float32).reshape(n, 4)
+        lib().oracle_tri_colors_mat(_p(normals), _p(d), n, _p(mat), _p(sh))
     return mat, sh
 
 

@@ -46,6 +46,24 @@ def test_host_tri_colors_equal_the_oracle():
     assert len(np.unique(sh)) > 20                   # shading varies with the normal
 
 
+def test_obj_materials_reach_the_colour_tables(tmp_path):
+    """mtllib/usemtl (MeshWavefrontIO.cc:114-200,385-395): per-submesh Kd and d, submeshes
+    flattened in order of first use (Scene.cc:63-82); faces before any usemtl get the default."""
+    open(os.path.join(tmp_path, "m.mtl"), "w").write(
+        "newmtl red\nKa 0 0 0\nKd 1 0 0\nd 0.5\n# comment\nnewmtl blue\nKd 0 0 1\n")
+    open(os.path.join(tmp_path, "s.obj"), "w").write(
+        "mtllib m.mtl\nv 0 0 0\nv 1 0 0\nv 0 1 0\nv 0 0 1\n"
+        "f 1 2 3\nusemtl blue\nf 1 2 4\nusemtl red\nf 1 3 4\nusemtl blue\nf 2 3 4\nusemtl nomtl\nf 1 3 2\n")
+    scene = mrt.Scene.from_obj(os.path.join(tmp_path, "s.obj"))
+    mat, sh = scene.tri_colors()
+    # flattened order: default submesh, blue (2 faces), red, nomtl (undefined -> default)
+    assert mat.tolist() == [GREY, 0xFFFF0000, 0xFFFF0000, 0x800000FF, GREY]   # d 0.5 -> 127.5 rounds to 128
+    diffuse = np.array([[.75, .75, .75, 1], [0, 0, 1, 1], [0, 0, 1, 1], [1, 0, 0, .5], [.75, .75, .75, 1]], np.float32)
+    omat, osh = O.tri_colors(scene.arrays()[2], diffuse)
+    assert np.array_equal(mat, omat) and np.array_equal(sh, osh)
+    assert (sh >> 24 == 255).all()                    # shaded colours are opaque (Scene.cc:80)
+
+
 def test_reconstruct_primary_known_answers():
     # two pixels traced in swapped order: slot 0 -> pixel 1 (hit tri 1), slot 1 -> pixel 0 (miss)
     shaded = np.array([0, 0xFF00FF00], np.uint32)
