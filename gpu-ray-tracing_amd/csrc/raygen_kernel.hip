@@ -131,37 +131,74 @@ __device__ inline uint32_t to_abgr(float4 v) {
            ((uint32_t)(fminf(fmaxf(v.w, 0.0f), 1.0f) * 255.0f) << 24);
 }
 
+__device__ inline void add_sample(float4& c, int tri, bool isPrimary, bool isAO, const uint32_t* shaded) {
+    float4 add;
+    if (tri == -1) add = isPrimary ? make_float4(0.2f, 0.4f, 0.8f, 1.0f) : make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+    else add = isAO ? make_float4(0.0f, 0.0f, 0.0f, 1.0f) : from_abgr(shaded[tri]);
+    c.x += add.x; c.y += add.y; c.z += add.z; c.w += add.w;
+}
+
+// Average -> AO background -> diffuse modulation -> one ABGR pixel (RendererKernels.cu:96-107).
+__device__ inline void finish_pixel(const ReconstructArgs& a, float4 c, int primarySlot) {
+    const float4 bg = make_float4(0.2f, 0.4f, 0.8f, 1.0f);
+    const float inv = 1.0f / (float)a.numRaysPerPrimary;
+    c.x *= inv; c.y *= inv; c.z *= inv; c.w *= inv;
+    const int tri = a.primaryResults[primarySlot].x;
+    if (a.rayType == MRT_RAY_AO && tri == -1) c = bg;
+    if (a.rayType == MRT_RAY_DIFFUSE) {
+        const float4 m = tri == -1 ? bg : from_abgr(a.triMaterialColor[tri]);
+        c.x *= m.x; c.y *= m.y; c.z *= m.z; c.w *= m.w;
+    }
+    a.pixels[a.primarySlotToId[primarySlot]] = to_abgr(c);
+}
+
 // One thread per primary ray of the batch: average the batch rays' colours
 // (background / white / shaded triangle colour), modulate by the primary hit's
 // material for diffuse, write one ABGR pixel (RendererKernels.cu:60-108).
-// Streaming: 16 B per result read + 4 B colour gathers (L2-resident tables), 4 B written.
+// General form: any batchIdToSlot (gathers), and the primary batch.
 __global__ __launch_bounds__(kThreads) void reconstruct_kernel(ReconstructArgs a) {
     const int task = (int)(blockIdx.x * kThreads + threadIdx.x);
     if (task >= a.numPrimary) return;
     const int n = a.numRaysPerPrimary;
     const bool isPrimary = a.rayType == MRT_RAY_PRIMARY, isAO = a.rayType == MRT_RAY_AO;
     const int primarySlot = a.firstPrimary + task;
-    const int primaryId = a.primarySlotToId[primarySlot];
-    const int batchBase = isPrimary ? primaryId : task * n;
-    const float4 bg = make_float4(0.2f, 0.4f, 0.8f, 1.0f);
+    const int batchBase = isPrimary ? a.primarySlotToId[primarySlot] : task * n;
     float4 c = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     for (int i = 0; i < n; i++) {
         const int slot = a.batchIdToSlot ? a.batchIdToSlot[batchBase + i] : (isPrimary ? primarySlot : batchBase + i);
-        const int tri = a.batchResults[slot].x;
-        float4 add;
-        if (tri == -1) add = isPrimary ? bg : make_float4(1.0f, 1.0f, 1.0f, 1.0f);
-        else add = isAO ? make_float4(0.0f, 0.0f, 0.0f, 1.0f) : from_abgr(a.triShadedColor[tri]);
-        c.x += add.x; c.y += add.y; c.z += add.z; c.w += add.w;
+        add_sample(c, a.batchResults[slot].x, isPrimary, isAO, a.triShadedColor);
     }
-    const float inv = 1.0f / (float)n;
-    c.x *= inv; c.y *= inv; c.z *= inv; c.w *= inv;
-    const int tri = a.primaryResults[primarySlot].x;
-    if (isAO && tri == -1) c = bg;
-    if (a.rayType == MRT_RAY_DIFFUSE) {
-        const float4 m = tri == -1 ? bg : from_abgr(a.triMaterialColor[tri]);
-        c.x *= m.x; c.y *= m.y; c.z *= m.z; c.w *= m.w;
+    finish_pixel(a, c, primarySlot);
+}
+
+// Identity-layout AO/diffuse batches (mrt_raygen_ao's): the block's n rays per
+// primary are one contiguous run of results, so the hit ids are staged through
+// LDS with coalesced loads (consecutive lanes, consecutive results) in tiles of
+// kTileSamples per primary, then each thread sums its own samples in ray order
+// (bit-identical to reconstruct_kernel). Row stride kTileSamples + 1 keeps the
+// per-thread LDS reads conflict-free.
+constexpr int kTileSamples = 16;
+__global__ __launch_bounds__(kThreads) void reconstruct_tiled_kernel(ReconstructArgs a) {
+    __shared__ int ids[kThreads * (kTileSamples + 1)];
+    const int n = a.numRaysPerPrimary;
+    const bool isAO = a.rayType == MRT_RAY_AO;
+    const int taskBase = (int)blockIdx.x * kThreads;
+    const int nTasks = min(kThreads, a.numPrimary - taskBase);
+    const int t = (int)threadIdx.x;
+    float4 c = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    for (int s0 = 0; s0 < n; s0 += kTileSamples) {
+        const int ns = min(kTileSamples, n - s0);
+        const int cnt = nTasks * ns;
+        __syncthreads();
+        for (int e = t; e < cnt; e += kThreads) {
+            const int tt = e / ns, ss = e - tt * ns;
+            ids[tt * (kTileSamples + 1) + ss] = a.batchResults[(int64_t)(taskBase + tt) * n + s0 + ss].x;
+        }
+        __syncthreads();
+        if (t < nTasks)
+            for (int ss = 0; ss < ns; ss++) add_sample(c, ids[t * (kTileSamples + 1) + ss], false, isAO, a.triShadedColor);
     }
-    a.pixels[primaryId] = to_abgr(c);
+    if (t < nTasks) finish_pixel(a, c, a.firstPrimary + taskBase + t);
 }
 
 int hip_fail(hipError_t e, const char* what) {
@@ -278,8 +315,11 @@ int mrt_reconstruct(int32_t rayType, int32_t numRaysPerPrimary, int32_t firstPri
     a.triMaterialColor = triMaterialColor;
     a.triShadedColor = triShadedColor;
     a.pixels = pixels;
-    hipLaunchKernelGGL(reconstruct_kernel, dim3((numPrimary + kThreads - 1) / kThreads), dim3(kThreads), 0,
-                       static_cast<hipStream_t>(stream), a);
+    const dim3 grid((numPrimary + kThreads - 1) / kThreads);
+    if (rayType != MRT_RAY_PRIMARY && !batchIdToSlot)
+        hipLaunchKernelGGL(reconstruct_tiled_kernel, grid, dim3(kThreads), 0, static_cast<hipStream_t>(stream), a);
+    else
+        hipLaunchKernelGGL(reconstruct_kernel, grid, dim3(kThreads), 0, static_cast<hipStream_t>(stream), a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MRT_OK : hip_fail(e, "reconstruct launch");
 }

@@ -227,3 +227,24 @@ def test_reference_compat_launchers(frame):
     blk = (C.c_int32 * 2)(32, 8)
     cnt = CountHitsInput(batch.size, batch.results.data_ptr(), 16)
     assert lib.launch_countHitsKernel(batch.size, blk, C.byref(cnt)) == g.count_hits(batch)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ray_type,samples", [(1, 20), (2, 17), (1, 3)])
+def test_tiled_and_gathering_paths_agree_on_ragged_frames(frame, ray_type, samples):
+    """The LDS-staged kernel (identity layout, tiles of 16 samples) against the gathering
+    kernel (explicit batchIdToSlot) and the oracle, on a frame that fills no block exactly."""
+    scene, cam, ao, bufs, t, g, rec = frame
+    w, h = 97, 33
+    prim, s2i = g.primary(cam, w, h)
+    t.trace_batch(prim)
+    batch = g.ao(prim, samples, ao if ray_type == 1 else cam.far, closest_hit=ray_type == 2)
+    t.trace_batch(batch)
+    tiled = rec.reconstruct(ray_type, prim, s2i, w * h, batch=batch, num_samples=samples).cpu().numpy()
+    ident = torch.arange(batch.size, dtype=torch.int32, device=prim.results.device)
+    gathered = rec.reconstruct(ray_type, prim, s2i, w * h, batch=batch, num_samples=samples,
+                               batch_id_to_slot=ident).cpu().numpy()
+    assert np.array_equal(tiled, gathered)
+    want = _oracle_pixels(scene, ray_type, samples, s2i.cpu().numpy(), prim.results_numpy(), batch.results_numpy(),
+                          w, h)
+    assert np.array_equal(tiled.view(np.uint32), want)
