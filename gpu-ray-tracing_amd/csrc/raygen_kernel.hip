@@ -75,6 +75,22 @@ __global__ __launch_bounds__(kThreads) void ao_kernel(AOArgs a) {
     }
 }
 
+// One thread per OUTPUT ray (numSamples > 1): consecutive lanes write consecutive
+// 32 B rays (coalesced), each recomputing its input ray's basis (a few dozen
+// ALU ops and three L2-resident reads). ao_sample(b, i) depends only on (b, i),
+// so the rays are the same bits as ao_kernel's.
+__global__ __launch_bounds__(kThreads) void ao_per_sample_kernel(AOArgs a) {
+    const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (gid >= (int64_t)a.numInput * a.numSamples) return;
+    const int task = (int)(gid / a.numSamples), i = (int)(gid - (int64_t)task * a.numSamples);
+    const int2 res = a.inResults[2 * task];
+    const rg::AOBasis b =
+        rg::ao_basis(a.inRays[task], res.x, __int_as_float(res.y), a.normals, a.numTris, a.seed, (uint32_t)task);
+    a.outRays[gid] = rg::ao_sample(b, i, a.maxDist);
+    if (a.outIdToSlot) a.outIdToSlot[gid] = (int32_t)gid;
+    if (a.outSlotToId) a.outSlotToId[gid] = (int32_t)gid;
+}
+
 // Per block: hits among its rays (id >= 0, RendererKernels.cu:131), one partial.
 __global__ __launch_bounds__(kThreads) void count_partial_kernel(const int4* results, int n, int perBlock,
                                                                 int32_t* partial) {
@@ -264,8 +280,14 @@ int mrt_raygen_ao(const void* inRays, const void* inResults, int32_t numInputRay
     a.outRays = static_cast<rg::RayRec*>(outRays);
     a.outIdToSlot = outIdToSlot;
     a.outSlotToId = outSlotToId;
-    hipLaunchKernelGGL(ao_kernel, dim3((numInputRays + kThreads - 1) / kThreads), dim3(kThreads), 0,
-                       static_cast<hipStream_t>(stream), a);
+    if (numSamples > 1) {
+        const int64_t total = (int64_t)numInputRays * numSamples;
+        hipLaunchKernelGGL(ao_per_sample_kernel, dim3((unsigned)((total + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                           static_cast<hipStream_t>(stream), a);
+    } else {
+        hipLaunchKernelGGL(ao_kernel, dim3((numInputRays + kThreads - 1) / kThreads), dim3(kThreads), 0,
+                           static_cast<hipStream_t>(stream), a);
+    }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MRT_OK : hip_fail(e, "raygen ao launch");
 }

@@ -105,3 +105,20 @@ def test_count_hits(gen, n):
     ids = np.where(rng.random(n) < 0.37, rng.integers(0, 1 << 30, n), -1).astype(np.int32)
     rb.results[:, 0] = torch.from_numpy(ids).cuda()
     assert gen().count_hits(rb) == int((ids >= 0).sum())
+
+
+def test_per_sample_ao_kernel_matches_the_per_ray_kernel(gen):
+    """numSamples > 1 runs one thread per output ray (coalesced writes); its sample 0 of
+    every input ray must be the per-ray kernel's (numSamples == 1) bits."""
+    from mrt.tracer import GpuBvh, Tracer
+    scene = mrt.Scene.synthetic("conference", 0, 1)
+    cam, ao = scene.camera()
+    t = Tracer(0)
+    t.set_bvh(GpuBvh(mrt.Bvh.build(scene).buffers()))
+    g = gen(scene)
+    prim, _ = g.primary(cam, 123, 45)
+    t.trace_batch(prim)
+    one = g.ao(prim, 1, ao).rays.cpu().numpy()
+    many = g.ao(prim, 7, ao).rays.cpu().numpy().reshape(-1, 7, 8)
+    assert np.array_equal(many[:, 0].view(np.uint32), one.view(np.uint32))
+    assert len(np.unique(many[:, :, 4])) > len(one)   # the other samples are distinct directions
