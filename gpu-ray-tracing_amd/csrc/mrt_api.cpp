@@ -6,6 +6,7 @@
 // ownership: CudaBVH.cc:101-109, RayBuffer.cc:42-81). It owns only its
 // workspace, sized for the persistent grid it launches.
 #include <hip/hip_runtime.h>
+#include <climits>
 
 #include <algorithm>
 #include <cstdio>
@@ -514,6 +515,32 @@ float launch_tracingKernel(int32_t nthreads, int32_t* blockSize, int numRays, bo
 void copy_tracing_results(void* result_host, void* result_dev, int32_t size) {
     const hipError_t e = hipMemcpy(result_host, result_dev, (size_t)size * 16u, hipMemcpyDeviceToHost);
     if (e != hipSuccess) compat_check(hipFail(e, "hipMemcpy"), __FILE__, __LINE__);
+}
+
+void launch_rayGenPrimaryKernel(int32_t nthreads, mrt_raygen_primary_input* in) {
+    (void)nthreads;
+    if (!in) compat_check(fail(MRT_ERR_INVALID_ARG, "null RayGenPrimaryInput"), __FILE__, __LINE__);
+    compat_check(mrt_raygen_primary(in->nscreenToWorld, in->origin, in->maxDist, in->w, in->h, in->indexToPixel,
+                                    in->rays, in->slotToID, in->idToSlot, nullptr),
+                 __FILE__, __LINE__);
+    const hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) compat_check(hipFail(e, "hipDeviceSynchronize"), __FILE__, __LINE__);
+}
+
+void launch_rayGenAOKernel(int32_t nthreads, mrt_raygen_ao_input* in) {
+    (void)nthreads;
+    if (!in || in->firstInputSlot < 0)
+        compat_check(fail(MRT_ERR_INVALID_ARG, "bad RayGenAOInput"), __FILE__, __LINE__);
+    // inSlot = taskIdx + firstInputSlot; the hash and the output slots use taskIdx (RayGenKernels.cu:128-131,163)
+    const char* inRays = static_cast<const char*>(in->inRays);
+    const char* inResults = static_cast<const char*>(in->inResults);
+    compat_check(mrt_raygen_ao(inRays ? inRays + (int64_t)in->firstInputSlot * 32 : nullptr,
+                               inResults ? inResults + (int64_t)in->firstInputSlot * 16 : nullptr, in->numInputRays,
+                               static_cast<const float*>(in->normals), INT64_MAX, in->numSamples, in->maxDist,
+                               in->randomSeed, in->outRays, in->outIDToSlot, in->outSlotToID, nullptr),
+                 __FILE__, __LINE__);
+    const hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) compat_check(hipFail(e, "hipDeviceSynchronize"), __FILE__, __LINE__);
 }
 
 void launch_reconstructKernel(int32_t nthreads, mrt_reconstruct_input* in) {

@@ -86,6 +86,8 @@ TRACE_SYMBOLS = [
     ("launch_tracingKernel", f32, [i32, vp, C.c_int, C.c_bool, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     ("copy_tracing_results", None, [vp, vp, i32]),
     ("launch_reconstructKernel", None, [i32, vp]),
+    ("launch_rayGenPrimaryKernel", None, [i32, vp]),
+    ("launch_rayGenAOKernel", None, [i32, vp]),
     ("launch_countHitsKernel", i32, [i32, vp, vp]),
 ]
 

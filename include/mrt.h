@@ -228,6 +228,35 @@ typedef struct mrt_count_hits_input {
     int32_t raysPerThread;
 } mrt_count_hits_input;
 
+/* RayGenKernels.hh:40-68 input structs, field for field: Vec3f = 3 floats, Mat4f =
+ * 16 floats column-major, then 8-byte-aligned pointers. */
+typedef struct mrt_raygen_primary_input {
+    float    origin[3];
+    float    nscreenToWorld[16];
+    int32_t  w, h;
+    float    maxDist;
+    void*    rays;
+    int32_t* idToSlot;
+    int32_t* slotToID;
+    int32_t* indexToPixel;
+} mrt_raygen_primary_input;
+
+typedef struct mrt_raygen_ao_input {
+    int32_t  firstInputSlot, numInputRays, numSamples;
+    float    maxDist;
+    uint32_t randomSeed;
+    void*    inRays;
+    void*    inResults;
+    void*    outRays;
+    int32_t* outIDToSlot;
+    int32_t* outSlotToID;
+    void*    normals;          /* const Vec3f*: one per triangle, unbounded like the reference's */
+} mrt_raygen_ao_input;
+
+/* launch_rayGenPrimaryKernel / launch_rayGenAOKernel (RayGenKernels.cu:295-330); blocking */
+void    launch_rayGenPrimaryKernel(int32_t nthreads, mrt_raygen_primary_input* in);
+void    launch_rayGenAOKernel(int32_t nthreads, mrt_raygen_ao_input* in);
+
 /* launch_reconstructKernel (RendererKernels.cu:166-186) */
 void    launch_reconstructKernel(int32_t nthreads, mrt_reconstruct_input* in);
 /* launch_countHitsKernel (RendererKernels.cu:189-215): returns the hit count */

@@ -248,3 +248,57 @@ def test_tiled_and_gathering_paths_agree_on_ragged_frames(frame, ray_type, sampl
     want = _oracle_pixels(scene, ray_type, samples, s2i.cpu().numpy(), prim.results_numpy(), batch.results_numpy(),
                           w, h)
     assert np.array_equal(tiled.view(np.uint32), want)
+
+
+class RayGenPrimaryInput(C.Structure):
+    """RayGenKernels.hh:40-51 (mrt.h mrt_raygen_primary_input)."""
+    _fields_ = [("origin", C.c_float * 3), ("nscreenToWorld", C.c_float * 16), ("w", C.c_int32), ("h", C.c_int32),
+                ("maxDist", C.c_float), ("rays", C.c_void_p), ("idToSlot", C.c_void_p), ("slotToID", C.c_void_p),
+                ("indexToPixel", C.c_void_p)]
+
+
+class RayGenAOInput(C.Structure):
+    """RayGenKernels.hh:55-68 (mrt.h mrt_raygen_ao_input)."""
+    _fields_ = [("firstInputSlot", C.c_int32), ("numInputRays", C.c_int32), ("numSamples", C.c_int32),
+                ("maxDist", C.c_float), ("randomSeed", C.c_uint32), ("inRays", C.c_void_p),
+                ("inResults", C.c_void_p), ("outRays", C.c_void_p), ("outIDToSlot", C.c_void_p),
+                ("outSlotToID", C.c_void_p), ("normals", C.c_void_p)]
+
+
+def test_raygen_input_struct_layout():
+    assert RayGenPrimaryInput.rays.offset == 88 and C.sizeof(RayGenPrimaryInput) == 120
+    assert RayGenAOInput.inRays.offset == 24 and C.sizeof(RayGenAOInput) == 72
+
+
+@pytest.mark.gpu
+def test_reference_compat_raygen_launchers(frame):
+    """launch_rayGenPrimaryKernel / launch_rayGenAOKernel (RayGen.cc:50-120 call shapes) produce
+    the same rays as the stream-ordered entry points; firstInputSlot offsets the input only."""
+    from mrt.raygen import nscreen_to_world
+    from mrt.tracer import RayBuffer
+    scene, cam, ao, bufs, t, g, rec = frame
+    w, h = 64, 40
+    dev = prim_dev = torch.device("cuda", 0)
+    want, want_s2i = g.primary(cam, w, h)
+    rays = torch.zeros((w * h, 8), dtype=torch.float32, device=dev)
+    s2i = torch.zeros(w * h, dtype=torch.int32, device=dev)
+    i2s = torch.zeros(w * h, dtype=torch.int32, device=dev)
+    table = torch.from_numpy(mrt.pixel_table(w, h)).to(dev)
+    inp = RayGenPrimaryInput((C.c_float * 3)(*cam.position), (C.c_float * 16)(*nscreen_to_world(cam, w, h)), w, h,
+                             float(cam.far), rays.data_ptr(), i2s.data_ptr(), s2i.data_ptr(), table.data_ptr())
+    lib = mrt._lib.trace_lib()
+    lib.launch_rayGenPrimaryKernel(w * h, C.byref(inp))
+    assert torch.equal(rays.view(torch.int32), want.rays.view(torch.int32)) and torch.equal(s2i, want_s2i)
+    assert torch.equal(i2s[s2i.long()], torch.arange(w * h, dtype=torch.int32, device=dev))
+    t.trace_batch(want)
+    first, n, samples = 100, 500, 3
+    sub = RayBuffer(want.rays[first:first + n].clone(), device=prim_dev)
+    sub.results.copy_(want.results[first:first + n])
+    expect = g.ao(sub, samples, ao).rays
+    out = torch.zeros((n * samples, 8), dtype=torch.float32, device=dev)
+    o2s = torch.zeros(n * samples, dtype=torch.int32, device=dev)
+    ainp = RayGenAOInput(first, n, samples, float(ao), mrt.AO_SEED, want.rays.data_ptr(), want.results.data_ptr(),
+                         out.data_ptr(), o2s.data_ptr(), None, g.normals.data_ptr())
+    lib.launch_rayGenAOKernel(n, C.byref(ainp))
+    assert torch.equal(out.view(torch.int32), expect.view(torch.int32))
+    assert torch.equal(o2s, torch.arange(n * samples, dtype=torch.int32, device=dev))
