@@ -375,8 +375,8 @@ def run_workload(name, tracer, world, rank, steps, warmup, exact, want_cpu, cach
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)   # 0.15 ms steps: 20 left clocks ramping (4.8-5.3 G vs 5.35 G stable)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default=HEADLINE, help="a WORKLOADS key or <scene>-<ray>-<W>x<H>")
     ap.add_argument("--rcp", default="exact", choices=["exact", "fast"],
                     help="exact = correctly rounded 1/x (bit-identical to the oracle); fast = v_rcp_f32")
