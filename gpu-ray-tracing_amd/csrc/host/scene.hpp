@@ -13,6 +13,7 @@ namespace mrt {
 struct Vec3i {
     int32_t x = 0, y = 0, z = 0;
     int32_t operator[](int i) const { return (&x)[i]; }
+    int32_t& operator[](int i) { return (&x)[i]; }
 };
 
 struct Camera {

@@ -14,9 +14,14 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/mrt.h"
 #include "trace_kernel.hpp"
+
+namespace mrt {
+struct Workspace;
+}
 
 struct mrt_tracer {
     int device = 0;
@@ -34,14 +39,11 @@ struct mrt_tracer {
 
     mrt_launch_cfg cfg{};
 
-    // Workspace.
-    unsigned* queues = nullptr;   // kMaxQueues * kQueueStrideWords words
-    int* status = nullptr;        // overflow counter
-    int* spill = nullptr;
-    size_t spillInts = 0;
-    unsigned* tailCount = nullptr;   // two record counters, used by alternate exporting launches
-    int* tailRec = nullptr;          // kTailWords x kTailCapacity words
-    unsigned tailEpoch = 0;          // exporting launches so far
+    // Launch scratch, one set per stream the handle has launched on: the stack
+    // spill slab, the queue heads and the overflow counter are written by a
+    // running trace, so two traces in flight on different streams must not
+    // share them (the handle's mutex only covers enqueueing).
+    std::vector<mrt::Workspace*> workspaces;
     hipEvent_t evStart = nullptr, evStop = nullptr;
 
     // Occupancy per kernel variant, queried once (hipOccupancy* is a host
@@ -61,6 +63,14 @@ int api_fail(int code, const std::string& what) {
     return code;
 }
 const char* api_last_error() { return g_lastError.c_str(); }
+
+struct Workspace {
+    void* stream = nullptr;       // the hipStream_t this scratch belongs to
+    unsigned* queues = nullptr;   // kMaxQueues * kQueueStrideWords words
+    int* status = nullptr;        // [0] = stack overflows since the last reset (sticky on the async path)
+    int* spill = nullptr;
+    size_t spillInts = 0;
+};
 }  // namespace mrt
 
 namespace {
@@ -90,13 +100,6 @@ struct DeviceGuard {
     }
 };
 
-// Tail export / resume defaults (profiles/round1_tuning.md, "Tail export").
-constexpr int kDefaultTailLanes = -1;
-constexpr int kDefaultTailAfterUs = 30;
-constexpr int kDefaultTailResumeLanes = 1;
-constexpr int kDefaultTailResumeWaves = 28;   // capped by the resume kernel's occupancy
-constexpr int kTailCapacity = 1 << 16;   // records (22 MB)
-
 mrt_launch_cfg default_cfg() {
     mrt_launch_cfg c;
     c.waves_per_cu = 0;   // auto: sized from the batch (grid_blocks)
@@ -105,10 +108,6 @@ mrt_launch_cfg default_cfg() {
     c.lds_stack = 16;
     c.schedule = 1;
     c.lane_groups = 1;
-    c.tail_lanes = kDefaultTailLanes;
-    c.tail_after_us = kDefaultTailAfterUs;
-    c.tail_resume_lanes = kDefaultTailResumeLanes;
-    c.tail_resume_waves = kDefaultTailResumeWaves;
     return c;
 }
 
@@ -116,10 +115,7 @@ bool valid_cfg(const mrt_launch_cfg& c) {
     return (c.waves_per_cu == 0 || (c.waves_per_cu >= 4 && c.waves_per_cu <= 32)) && c.fetch_threshold >= 0 && c.fetch_threshold <= 64 &&
            (c.num_queues == -1 || (c.num_queues >= 1 && c.num_queues <= mrt::kMaxQueues)) &&
            (c.lds_stack == 8 || c.lds_stack == 16 || c.lds_stack == 32) && (c.schedule == 1 || c.schedule == 2) &&
-           c.lane_groups >= 1 && c.lane_groups <= 64 && (c.lane_groups & (c.lane_groups - 1)) == 0 &&
-           (c.tail_lanes == -1 || (c.tail_lanes >= 1 && c.tail_lanes <= 64)) && c.tail_after_us >= 1 &&
-           c.tail_after_us <= 100000 && c.tail_resume_lanes >= 1 && c.tail_resume_lanes <= 64 &&
-           c.tail_resume_waves >= 4 && c.tail_resume_waves <= 32 && c.tail_resume_waves % 4 == 0;
+           c.lane_groups >= 1 && c.lane_groups <= 64 && (c.lane_groups & (c.lane_groups - 1)) == 0;
 }
 
 mrt::TraceVariant variant_for(const mrt_tracer* t, uint32_t flags) {
@@ -150,7 +146,7 @@ constexpr int kAutoMinWaves = 8;
 int variant_key(const mrt::TraceVariant& v) {
     const int lds = v.ldsStack == 8 ? 0 : v.ldsStack == 16 ? 1 : 2;
     return (v.anyHit ? 1 : 0) | (v.speculative ? 2 : 0) | (v.exactRcp ? 4 : 0) | (v.stats ? 8 : 0) | (lds << 4) |
-           (v.ifif ? 64 : 0) | (v.resume ? 128 : 0);
+           (v.ifif ? 64 : 0);
 }
 
 int grid_blocks(mrt_tracer* t, const mrt::TraceVariant& v, int numRays, int* outBlocksPerCU) {
@@ -178,31 +174,41 @@ int grid_blocks(mrt_tracer* t, const mrt::TraceVariant& v, int numRays, int* out
     return perCU * t->numCUs;
 }
 
-int ensure_workspace(mrt_tracer* t, int totalLanes, int ldsStack, bool tail) {
-    if (!t->queues) {
-        MRT_HIP(hipMalloc(&t->queues, mrt::kMaxQueues * mrt::kQueueStrideWords * sizeof(unsigned)));
-        MRT_HIP(hipMalloc(&t->status, 64 * sizeof(int)));
-        MRT_HIP(hipMemset(t->status, 0, 64 * sizeof(int)));
+// The scratch of `stream` (created on first use), grown to the grid's spill slab.
+int workspace_for(mrt_tracer* t, void* stream, int totalLanes, int ldsStack, mrt::Workspace** out) {
+    mrt::Workspace* w = nullptr;
+    for (mrt::Workspace* x : t->workspaces)
+        if (x->stream == stream) w = x;
+    if (!w) {
+        w = new mrt::Workspace();
+        w->stream = stream;
+        t->workspaces.push_back(w);
+        MRT_HIP(hipMalloc(&w->queues, mrt::kMaxQueues * mrt::kQueueStrideWords * sizeof(unsigned)));
+        MRT_HIP(hipMalloc(&w->status, 64 * sizeof(int)));
+        MRT_HIP(hipMemset(w->status, 0, 64 * sizeof(int)));
     }
     const size_t need = (size_t)(mrt::kStackCapacity - ldsStack) * (size_t)totalLanes;
-    if (need > t->spillInts) {
-        if (t->spill) MRT_HIP(hipFree(t->spill));
-        t->spill = nullptr;
-        t->spillInts = 0;
-        MRT_HIP(hipMalloc(&t->spill, need * sizeof(int)));
-        t->spillInts = need;
-    }
-    if (tail && !t->tailCount) {
-        MRT_HIP(hipMalloc(&t->tailCount, 2 * sizeof(unsigned)));
-        MRT_HIP(hipMemset(t->tailCount, 0, 2 * sizeof(unsigned)));
-        MRT_HIP(hipMalloc(&t->tailRec, (size_t)mrt::kTailWords * kTailCapacity * sizeof(int)));
+    if (need > w->spillInts) {
+        // A smaller slab may still be in use by this stream's previous launch.
+        MRT_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+        if (w->spill) MRT_HIP(hipFree(w->spill));
+        w->spill = nullptr;
+        w->spillInts = 0;
+        MRT_HIP(hipMalloc(&w->spill, need * sizeof(int)));
+        w->spillInts = need;
     }
     if (!t->evStart) {
         MRT_HIP(hipEventCreate(&t->evStart));
         MRT_HIP(hipEventCreate(&t->evStop));
     }
+    *out = w;
     return MRT_OK;
 }
+
+// Largest batch one launch takes: ray/result addressing and the strided round
+// arithmetic stay inside int32 with room for the grid (bigger batches are split
+// by the caller, as the reference Renderer does at 2^21 rays, Renderer.cc:46).
+constexpr int32_t kMaxRaysPerLaunch = 1 << 30;
 
 int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, uint32_t flags, int32_t* stats,
                void* stream, mrt_trace_info* info) {
@@ -216,24 +222,15 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     if (!rays || !results) return fail(MRT_ERR_INVALID_ARG, "null ray/result buffer");
     if ((flags & MRT_TRACE_STATS) && !stats) return fail(MRT_ERR_INVALID_ARG, "MRT_TRACE_STATS without stats buffer");
 
+    if (numRays > kMaxRaysPerLaunch) return fail(MRT_ERR_TOO_LARGE, "more than 2^30 rays in one launch: split the batch");
+
     DeviceGuard guard(t->device);
     const mrt::TraceVariant v = variant_for(t, flags);
     int perCU = 0;
     const int blocks = grid_blocks(t, v, numRays, &perCU);
     const int totalLanes = blocks * mrt::kBlockThreads;
-    // Tail export / resume: while-while launches only. The resume pass uses at
-    // most the first pass's grid (so the spill slab fits both).
-    const bool tail = !v.ifif && t->cfg.tail_lanes > 0;
-    mrt::TraceVariant vr = v;
-    vr.resume = true;
-    int resumeBlocks = 0;
-    if (tail) {
-        int occ = t->occ[variant_key(vr)];
-        if (occ <= 0 && (mrt::trace_occupancy(vr, &occ) != hipSuccess || occ <= 0)) occ = 1;
-        t->occ[variant_key(vr)] = occ;
-        resumeBlocks = std::min(blocks, std::min(occ, t->cfg.tail_resume_waves / 4) * t->numCUs);
-    }
-    if (int rc = ensure_workspace(t, totalLanes, v.ldsStack, tail)) return rc;
+    mrt::Workspace* ws = nullptr;
+    if (int rc = workspace_for(t, stream, totalLanes, v.ldsStack, &ws)) return rc;
 
     mrt::TraceArgs a{};
     a.rays = static_cast<const float4*>(rays);
@@ -248,32 +245,20 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     a.fetchThreshold = t->cfg.fetch_threshold;
     a.laneGroupsLog2 = __builtin_ctz((unsigned)t->cfg.lane_groups);
     a.totalLanes = totalLanes;
-    a.queues = t->queues;
-    a.spill = t->spill;
-    a.status = t->status;
+    a.queues = ws->queues;
+    a.spill = ws->spill;
+    a.status = ws->status;
     a.stats = reinterpret_cast<int4*>(stats);
-    if (tail) {
-        ++t->tailEpoch;
-        a.tailLanes = t->cfg.tail_lanes;
-        a.tailAfter = t->cfg.tail_after_us * 100;   // s_memrealtime runs at 100 MHz
-        a.tailResumeLanes = t->cfg.tail_resume_lanes;
-        a.tailCapacity = kTailCapacity;
-        a.tailCount = t->tailCount + (t->tailEpoch & 1u);
-        a.tailCountNext = t->tailCount + ((t->tailEpoch + 1u) & 1u);
-        a.tailRec = t->tailRec;
-    }
 
     hipStream_t s = static_cast<hipStream_t>(stream);
     // Queue heads restart at zero for every launch; strided mode has none.
     if (a.numQueues > 0)
-        MRT_HIP(hipMemsetAsync(t->queues, 0, mrt::kMaxQueues * mrt::kQueueStrideWords * sizeof(unsigned), s));
+        MRT_HIP(hipMemsetAsync(ws->queues, 0, mrt::kMaxQueues * mrt::kQueueStrideWords * sizeof(unsigned), s));
+    // The blocking call reports this launch's overflows alone; the asynchronous
+    // one leaves the counter sticky (mrt_tracer_stack_overflows reads it).
+    if (info) MRT_HIP(hipMemsetAsync(ws->status, 0, sizeof(int), s));
     if (info) MRT_HIP(hipEventRecord(t->evStart, s));
     MRT_HIP(mrt::launch_trace(v, a, blocks, s));
-    if (tail) {
-        mrt::TraceArgs r = a;
-        r.totalLanes = resumeBlocks * mrt::kBlockThreads;
-        MRT_HIP(mrt::launch_trace(vr, r, resumeBlocks, s));
-    }
     if (info) {
         MRT_HIP(hipEventRecord(t->evStop, s));
         MRT_HIP(hipEventSynchronize(t->evStop));
@@ -283,13 +268,12 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
         info->lds_stack_entries = v.ldsStack;
         info->schedule = v.ifif ? 2 : 1;
         int overflow = 0;
-        MRT_HIP(hipMemcpy(&overflow, t->status, sizeof(int), hipMemcpyDeviceToHost));
+        MRT_HIP(hipMemcpy(&overflow, ws->status, sizeof(int), hipMemcpyDeviceToHost));
         info->stack_overflows = overflow;
-        if (tail) {
-            unsigned n = 0;
-            MRT_HIP(hipMemcpy(&n, a.tailCount, sizeof(n), hipMemcpyDeviceToHost));
-            info->tail_records = (int32_t)n;
-        }
+        if (overflow)
+            return fail(MRT_ERR_STACK_OVERFLOW, std::to_string(overflow) +
+                                                    " stack pushes past the 64-entry traversal stack: those rays' "
+                                                    "results are incomplete (BVH deeper than the reference's STACK_SIZE)");
     }
     return MRT_OK;
 }
@@ -338,7 +322,8 @@ const char* mrt_error_string(int err) {
         case MRT_ERR_NOT_BOUND: return "no BVH bound";
         case MRT_ERR_HIP: return "HIP runtime error";
         case MRT_ERR_NO_DEVICE: return "no HIP device";
-        case MRT_ERR_TOO_LARGE: return "buffer larger than 4 GiB";
+        case MRT_ERR_TOO_LARGE: return "buffer or batch too large";
+        case MRT_ERR_STACK_OVERFLOW: return "traversal stack overflow";
         default: return "unknown error";
     }
 }
@@ -385,11 +370,13 @@ int mrt_tracer_destroy(mrt_tracer* t) {
     if (!t) return MRT_OK;
     {
         DeviceGuard guard(t->device);
-        if (t->queues) (void)hipFree(t->queues);
-        if (t->status) (void)hipFree(t->status);
-        if (t->spill) (void)hipFree(t->spill);
-        if (t->tailCount) (void)hipFree(t->tailCount);
-        if (t->tailRec) (void)hipFree(t->tailRec);
+        for (mrt::Workspace* w : t->workspaces) {
+            if (w->stream) (void)hipStreamSynchronize(static_cast<hipStream_t>(w->stream));
+            if (w->queues) (void)hipFree(w->queues);
+            if (w->status) (void)hipFree(w->status);
+            if (w->spill) (void)hipFree(w->spill);
+            delete w;
+        }
         if (t->evStart) (void)hipEventDestroy(t->evStart);
         if (t->evStop) (void)hipEventDestroy(t->evStop);
     }
@@ -435,10 +422,6 @@ int mrt_tracer_set_config(mrt_tracer* t, const mrt_launch_cfg* cfg) {
     if (c.lds_stack == 0) c.lds_stack = d.lds_stack;
     if (c.schedule == 0) c.schedule = d.schedule;
     if (c.lane_groups == 0) c.lane_groups = d.lane_groups;
-    if (c.tail_lanes == 0) c.tail_lanes = d.tail_lanes;
-    if (c.tail_after_us == 0) c.tail_after_us = d.tail_after_us;
-    if (c.tail_resume_lanes == 0) c.tail_resume_lanes = d.tail_resume_lanes;
-    if (c.tail_resume_waves == 0) c.tail_resume_waves = d.tail_resume_waves;
     if (!valid_cfg(c)) return fail(MRT_ERR_INVALID_ARG, "launch config out of range");
     std::lock_guard<std::mutex> lock(t->mu);
     t->cfg = c;
@@ -460,6 +443,22 @@ int mrt_tracer_trace_timed(mrt_tracer* t, const void* rays, void* results, int32
                            int32_t* stats, void* stream, mrt_trace_info* info) {
     mrt_trace_info local;
     return trace_impl(t, rays, results, numRays, flags, stats, stream, info ? info : &local);
+}
+
+int mrt_tracer_stack_overflows(mrt_tracer* t, int64_t* count, int32_t reset) {
+    if (!t || !count) return fail(MRT_ERR_INVALID_ARG, "null argument");
+    std::lock_guard<std::mutex> lock(t->mu);
+    DeviceGuard guard(t->device);
+    int64_t total = 0;
+    for (mrt::Workspace* w : t->workspaces) {
+        int n = 0;
+        MRT_HIP(hipStreamSynchronize(static_cast<hipStream_t>(w->stream)));
+        MRT_HIP(hipMemcpy(&n, w->status, sizeof(int), hipMemcpyDeviceToHost));
+        total += n;
+        if (reset) MRT_HIP(hipMemset(w->status, 0, sizeof(int)));
+    }
+    *count = total;
+    return MRT_OK;
 }
 
 int mrt_bind_bvh(const void* nodes, int64_t nodeBytes, const void* woop, int64_t woopBytes,

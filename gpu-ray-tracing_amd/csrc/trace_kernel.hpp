@@ -38,20 +38,9 @@ struct TraceArgs {
     int totalLanes;            // grid lanes (stride of the spill slab)
     unsigned* queues;          // numQueues heads, kQueueStrideWords apart, zeroed per launch
     int* spill;                // (kStackCapacity - S) * totalLanes ints
-    int* status;               // [0] = stack overflow count
+    int* status;               // [0] = stack overflow count (lanes that pushed past kStackCapacity)
     int4* stats;               // per-ray {nodes, tris, leaves, 0} (STATS variants)
-    // Tail export / resume (trace_kernel.hip): tailLanes == 0: off.
-    int tailLanes;             // pass 1: a wave exports its traversing lanes when at most this many are left ...
-    int tailAfter;             // ... and its current round has run this many 10-ns ticks
-    int tailResumeLanes;       // pass 2: lanes per wave resuming records
-    int tailCapacity;          // records the slab holds
-    unsigned* tailCount;       // records written by pass 1 (zeroed by the previous exporting launch)
-    unsigned* tailCountNext;   // the counter of the next exporting launch: pass 1 zeroes it
-    int* tailRec;              // kTailWords x tailCapacity words, word-major
 };
-
-constexpr int kTailFixedWords = 20;   // lane state (18 used), then the stack
-constexpr int kTailWords = kTailFixedWords + kStackCapacity;
 
 // Variant selector (all combinations are instantiated in trace_kernel.hip).
 struct TraceVariant {
@@ -61,7 +50,6 @@ struct TraceVariant {
     bool stats;
     int ldsStack;       // 8, 16 or 32 LDS entries per lane
     bool ifif;          // if-if scheduling (one node or triangle step per lane per pass) vs while-while
-    bool resume = false;   // the tail resume pass (reads records instead of rays)
 };
 
 // Launch one persistent trace. grid = number of 256-thread workgroups.

@@ -44,7 +44,9 @@ enum {
     MRT_ERR_NOT_BOUND = 2,     /* trace before bind (CudaTracer.cc:129)      */
     MRT_ERR_HIP = 3,           /* a HIP runtime call failed                  */
     MRT_ERR_NO_DEVICE = 4,     /* no GPU visible                             */
-    MRT_ERR_TOO_LARGE = 5      /* buffer beyond the 4 GiB buffer-offset range */
+    MRT_ERR_TOO_LARGE = 5,     /* buffer beyond the 4 GiB buffer-offset range, or > 2^30 rays per launch */
+    MRT_ERR_STACK_OVERFLOW = 6 /* a ray needed more than the reference's 64 stack entries
+                                  (kepler_dynamic_fetch.cu:47 STACK_SIZE): its result is incomplete */
 };
 
 /* ---- trace flags (bit set) -------------------------------------------- */
@@ -57,7 +59,10 @@ enum {
     MRT_TRACE_STATS = 1u << 3     /* also write per-ray {inner nodes, tris tested, leaves, latency in 10 ns ticks} int4s */
 };
 
-typedef struct mrt_tracer mrt_tracer;   /* one per HIP device; re-entrant per handle */
+/* One per HIP device. Re-entrant: launches on different streams get separate
+ * scratch (stack spill slab, queue heads, overflow counter), so traces on
+ * several streams of one handle may run concurrently. */
+typedef struct mrt_tracer mrt_tracer;
 
 /* Tuning knobs of the persistent launch (0 = library default). */
 typedef struct mrt_launch_cfg {
@@ -75,15 +80,6 @@ typedef struct mrt_launch_cfg {
                                   divergent waves (profiles/round1_tuning.md). 0 = library default */
     int32_t lane_groups;       /* strided mode: a wave's 64 lanes take rays from this many (1..64, power of
                                   two) distant sub-ranges of the batch instead of 64 consecutive rays */
-    int32_t tail_lanes;        /* while-while only: a wave whose current round has run tail_after_us and is
-                                  down to at most this many (1..64) traversing lanes writes each lane's state
-                                  (ray, hit so far, node, stack) to a tail slab and drops it; a second launch
-                                  on the same stream resumes those lanes tail_resume_lanes per wave, spread
-                                  over all CUs. Results unchanged. -1 = off, 0 = library default */
-    int32_t tail_after_us;     /* see tail_lanes (1..100000 microseconds; 0 = library default)   */
-    int32_t tail_resume_lanes; /* see tail_lanes (1..64 lanes per resuming wave; 0 = library default) */
-    int32_t tail_resume_waves; /* see tail_lanes: resuming waves per CU (4..32, a multiple of 4; 0 = library
-                                  default). Few waves per CU give each resumed lane a SIMD of its own */
 } mrt_launch_cfg;
 
 /* Per-launch statistics reported back to the host (optional). */
@@ -92,9 +88,9 @@ typedef struct mrt_trace_info {
     int32_t grid_waves;        /* persistent waves launched                                       */
     int32_t block_threads;     /* threads per workgroup                                           */
     int32_t lds_stack_entries; /* per-lane traversal-stack entries held in LDS                    */
-    int32_t stack_overflows;   /* lanes that needed more than 64 stack entries (0 for SBVH depth<=64) */
+    int32_t stack_overflows;   /* pushes past the 64-entry stack in this launch (then the call returns
+                                  MRT_ERR_STACK_OVERFLOW; 0 for any SBVH of depth <= 64)            */
     int32_t schedule;          /* traversal schedule the launch used (1 while-while, 2 if-if)     */
-    int32_t tail_records;      /* lanes exported to the tail resume pass (tail_lanes; 0 when off) */
 } mrt_trace_info;
 
 /* ---- handle API -------------------------------------------------------- */
@@ -113,16 +109,24 @@ int  mrt_tracer_unbind(mrt_tracer* t);
 int  mrt_tracer_set_config(mrt_tracer* t, const mrt_launch_cfg* cfg);
 int  mrt_tracer_get_config(const mrt_tracer* t, mrt_launch_cfg* cfg);
 
-/* Stream-ordered trace of numRays rays (device pointers). stream is a
+/* Stream-ordered trace of numRays (<= 2^30) rays (device pointers). stream is a
  * hipStream_t (NULL = the null stream). stats may be NULL unless
- * MRT_TRACE_STATS is set (then: int32[4*numRays]). Asynchronous. */
+ * MRT_TRACE_STATS is set (then: int32[4*numRays]). Asynchronous: a stack
+ * overflow cannot be returned here; it accumulates in a sticky per-stream
+ * counter that mrt_tracer_stack_overflows reads. */
 int  mrt_tracer_trace(mrt_tracer* t, const void* rays, void* results, int32_t numRays,
                       uint32_t flags, int32_t* stats, void* stream);
 
 /* Same, but blocking and event-timed around the launch only — the
- * reference's launch_tracingKernel contract (kepler_dynamic_fetch.cu:432-474). */
+ * reference's launch_tracingKernel contract (kepler_dynamic_fetch.cu:432-474).
+ * Returns MRT_ERR_STACK_OVERFLOW (results written, info filled) when a ray of
+ * this launch needed more than 64 stack entries. */
 int  mrt_tracer_trace_timed(mrt_tracer* t, const void* rays, void* results, int32_t numRays,
                             uint32_t flags, int32_t* stats, void* stream, mrt_trace_info* info);
+
+/* Stack overflows of asynchronous launches since the last reset, summed over the
+ * handle's streams (synchronises them). reset != 0 zeroes the counters. */
+int  mrt_tracer_stack_overflows(mrt_tracer* t, int64_t* count, int32_t reset);
 
 /* Diagnostics: run the EXACT variants' reciprocal (v_rcp_f32 + one FMA Newton step)
  * against the correctly rounded 1.0f / x for all 2^32 inputs on the current device;

@@ -134,3 +134,32 @@ def cases():
     out.append(("deep: tmin=2.5 -> farthest", deep, [ray((0.25, 0.25, 0), down, tmin=2.5)], False, [(11, 3.0)]))
     out.append(("deep: from below, nearest is 11", deep, [ray((0.25, 0.25, -5), (0, 0, 1))], False, [(11, 2.0)]))
     return out
+
+
+def scene_comb(depth):
+    """A comb of `depth` inner nodes for a stack-depth test (reference STACK_SIZE 64,
+    kepler_dynamic_fetch.cu:47). Inner node k (k < depth-1) has child 0 = inner
+    node k+1 (its box entered at t = k + 1.5) and child 1 = leaf k (entered at
+    t = k + 2), so a ray down -z through (0.25, 0.25) goes near and pushes one
+    leaf per level: `depth` pushes before the first pop. Leaf k holds triangle k
+    in the plane z = -(k+1) (t = k + 2); the last inner node holds leaves
+    depth-1 and depth. Closest hit: triangle 0 at t = 2 (hand answer).
+    Returns (buffers, ray, (id, t))."""
+    b = Compact2Builder()
+    inner = [b.reserve_inner() for _ in range(depth)]
+    bottom = -(depth + 2.0)
+
+    def tri_leaf(k):
+        z = -(k + 1.0)
+        return b.leaf([(k, (0, 0, z), (1, 0, z), (0, 1, z))])
+
+    def leaf_box(k):
+        return ((0, 0, -(k + 1.0)), (1, 1, -(k + 1.0)))
+
+    for k in range(depth - 1, -1, -1):
+        if k == depth - 1:
+            b.set_inner(inner[k], leaf_box(k), leaf_box(k + 1), tri_leaf(k), tri_leaf(k + 1))
+        else:
+            child_box = ((0, 0, bottom), (1, 1, -(k + 1.0) + 0.5))
+            b.set_inner(inner[k], child_box, leaf_box(k), inner[k + 1] * 4, tri_leaf(k))
+    return b.buffers(), ray((0.25, 0.25, 1), (0, 0, -1), tmax=1000.0), (0, 2.0)

@@ -47,8 +47,9 @@ def test_host_tri_colors_equal_the_oracle():
 
 
 def test_obj_materials_reach_the_colour_tables(tmp_path):
-    """mtllib/usemtl (MeshWavefrontIO.cc:114-200,385-395): per-submesh Kd and d, submeshes
-    flattened in order of first use (Scene.cc:63-82); faces before any usemtl get the default."""
+    """mtllib/usemtl (MeshWavefrontIO.cc:114-200,366-384): per-submesh Kd and d, submeshes
+    flattened in order of creation (Scene.cc:63-82); faces before any usemtl, and faces after
+    a usemtl naming no loaded material, join the default submesh."""
     open(os.path.join(tmp_path, "m.mtl"), "w").write(
         "newmtl red\nKa 0 0 0\nKd 1 0 0\nd 0.5\n# comment\nnewmtl blue\nKd 0 0 1\n")
     open(os.path.join(tmp_path, "s.obj"), "w").write(
@@ -56,12 +57,32 @@ def test_obj_materials_reach_the_colour_tables(tmp_path):
         "f 1 2 3\nusemtl blue\nf 1 2 4\nusemtl red\nf 1 3 4\nusemtl blue\nf 2 3 4\nusemtl nomtl\nf 1 3 2\n")
     scene = mrt.Scene.from_obj(os.path.join(tmp_path, "s.obj"))
     mat, sh = scene.tri_colors()
-    # flattened order: default submesh, blue (2 faces), red, nomtl (undefined -> default)
-    assert mat.tolist() == [GREY, 0xFFFF0000, 0xFFFF0000, 0x800000FF, GREY]   # d 0.5 -> 127.5 rounds to 128
-    diffuse = np.array([[.75, .75, .75, 1], [0, 0, 1, 1], [0, 0, 1, 1], [1, 0, 0, .5], [.75, .75, .75, 1]], np.float32)
+    # flattened order: default submesh (faces 1 and 5: 'nomtl' is undefined), blue (faces 2, 4), red (face 3)
+    assert mat.tolist() == [GREY, GREY, 0xFFFF0000, 0xFFFF0000, 0x800000FF]   # d 0.5 -> 127.5 rounds to 128
+    _, tris, _ = scene.arrays()
+    assert tris.tolist() == [[0, 1, 2], [0, 2, 1], [0, 1, 3], [1, 2, 3], [0, 2, 3]]
+    diffuse = np.array([[.75, .75, .75, 1], [.75, .75, .75, 1], [0, 0, 1, 1], [0, 0, 1, 1], [1, 0, 0, .5]], np.float32)
     omat, osh = O.tri_colors(scene.arrays()[2], diffuse)
     assert np.array_equal(mat, omat) and np.array_equal(sh, osh)
     assert (sh >> 24 == 255).all()                    # shaded colours are opaque (Scene.cc:80)
+
+
+def test_obj_without_material_library_and_bad_indices(tmp_path):
+    """MeshWavefrontIO.cc:317-384: with no mtllib every usemtl names an unknown material, so
+    all faces stay in the default submesh in file order; a face index outside the vertex list
+    becomes the reference's vertex -1 (position 0,0,0); a 'v' line with four values is invalid
+    and skipped (it takes no index); an unparsable face is skipped."""
+    open(os.path.join(tmp_path, "s.obj"), "w").write(
+        "v 1 1 1\nv 1 0 0 1\nv 2 0 0\nv 0 2 0\nusemtl red\nf 1 2 3\nusemtl blue\nf 1 3 9\nf 1 x 3\nf -3 -2 -1\n")
+    scene = mrt.Scene.from_obj(os.path.join(tmp_path, "s.obj"))
+    v, t, _ = scene.arrays()
+    assert scene.num_triangles == 3
+    pos = v[t]   # (tri, corner, xyz)
+    assert pos.tolist() == [[[1, 1, 1], [2, 0, 0], [0, 2, 0]],
+                            [[1, 1, 1], [0, 2, 0], [0, 0, 0]],
+                            [[1, 1, 1], [2, 0, 0], [0, 2, 0]]]
+    mat, _ = scene.tri_colors()
+    assert (mat == GREY).all()
 
 
 def test_reconstruct_primary_known_answers():

@@ -221,52 +221,73 @@ def test_if_if_deep_stacks_and_rebinding(tracer):
         tracer.set_config(**saved)
 
 
-# ---------------------------------------------------------------- tail export / resume
-TAIL_CFGS = [dict(tail_lanes=64, tail_after_us=1), dict(tail_lanes=64, tail_after_us=1, tail_resume_lanes=64),
-             dict(tail_lanes=64, tail_after_us=1, lds_stack=8, tail_resume_lanes=3),
-             dict(tail_lanes=8, tail_after_us=2, waves_per_cu=4), dict(tail_lanes=64, tail_after_us=1, lane_groups=8),
-             dict(tail_lanes=64, tail_after_us=1, tail_resume_waves=4, tail_resume_lanes=2)]
-
-
-@pytest.mark.parametrize("cfg", TAIL_CFGS, ids=lambda c: ",".join(f"{k}={v}" for k, v in c.items()))
-@pytest.mark.parametrize("wl", WORKLOADS, ids=lambda w: "-".join(map(str, w)))
-def test_tail_export_resume_is_bit_identical(tracer, wl, cfg):
-    """Lanes exported mid-traversal (state + stack) and resumed by the second launch
-    give the oracle's results and per-ray counters exactly (per-lane order), and the
-    speculative mode's closest hits exactly; a 1-us threshold exports most lanes."""
-    bufs, rays, any_hit, want, st = scene_setup(*wl)
+# ---------------------------------------------------------------- concurrency, overflow, limits
+def test_concurrent_streams_on_one_handle(tracer):
+    """two traces of one handle in flight on two streams at once, on a deep
+    scene whose stacks spill past an 8-entry LDS ring: each stream has its own spill
+    slab / counters, so both batches equal the oracle."""
+    from mrt.tracer import GpuBvh, RayBuffer
+    bufs_a, rays_a, _, want_a, _ = scene_setup("hairball:800", 256, 192, "diffuse")
     saved = tracer.config()
     try:
-        tracer.set_config(**cfg)
-        res, gst = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=False, stats=True)
-        exported = tracer.last_info["tail_records"]
-        assert np.array_equal(res[:, :2], want[:, :2]) and np.array_equal(gst[:, :3], st[:, :3])
-        res2, _ = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=True)
-        if any_hit:
-            assert_valid_hits(rays, res2, want, bufs)
+        tracer.set_config(lds_stack=8)
+        tracer.set_bvh(GpuBvh(bufs_a))
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        rbs = [RayBuffer(rays_a, need_closest_hit=True) for _ in range(4)]
+        torch.cuda.synchronize()
+        for k, rb in enumerate(rbs):
+            s = s1 if k % 2 == 0 else s2
+            with torch.cuda.stream(s):
+                tracer.trace_async(rb, exact_rcp=True, speculative=False, stream=s)
+        s1.synchronize()
+        s2.synchronize()
+        for rb in rbs:
+            assert np.array_equal(rb.results_numpy()[:, :2], want_a[:, :2])
+    finally:
+        tracer.set_config(**saved)
+
+
+@pytest.mark.parametrize("depth,overflow", [(40, False), (63, False), (64, True), (70, True)])
+def test_stack_overflow_is_reported(tracer, depth, overflow):
+    """A comb BVH whose ray pushes one far leaf per level (kat.scene_comb): with 70
+    levels the reference's 64-entry stack (kepler_dynamic_fetch.cu:47) overflows.
+    The blocking trace reports it (MRT_ERR_STACK_OVERFLOW + per-launch count), the
+    async path keeps a sticky counter; up to 63 pushes (the reference's capacity: sentinel +
+    63) trace exactly to the hand answer, through the spill slab."""
+    from mrt import _lib
+    from mrt.tracer import GpuBvh, RayBuffer
+    bufs, ray, expect = kat.scene_comb(depth)
+    tracer.set_bvh(GpuBvh(bufs))
+    n0 = C.c_int64()
+    _lib.check(tracer.lib.mrt_tracer_stack_overflows(tracer._h, C.byref(n0), 1))
+    rb = RayBuffer(np.stack([ray] * 64), need_closest_hit=True)
+    for spec in (False, True):
+        if overflow:
+            with pytest.raises(_lib.MrtError, match="stack overflow"):
+                tracer.trace_batch(rb, exact_rcp=True, speculative=spec)
+            assert tracer.lib.mrt_tracer_trace_timed(tracer._h, rb.rays.data_ptr(), rb.results.data_ptr(), rb.size,
+                                                     _lib.MRT_TRACE_EXACT_RCP, None, None,
+                                                     C.byref(_lib.TraceInfo())) == _lib.MRT_ERR_STACK_OVERFLOW
         else:
-            assert np.array_equal(res2[:, :2], want[:, :2])
-        if cfg["tail_lanes"] == 64:
-            assert exported > 0, "the 1-us threshold exported nothing: the resume pass went untested"
-    finally:
-        tracer.set_config(**saved)
+            tracer.trace_batch(rb, exact_rcp=True, speculative=spec)
+            res = rb.results_numpy()
+            assert (res[:, 0] == expect[0]).all() and (res[:, 1] == kat.f2i(expect[1])).all()
+    tracer.trace_async(rb, exact_rcp=True)
+    n = C.c_int64()
+    _lib.check(tracer.lib.mrt_tracer_stack_overflows(tracer._h, C.byref(n), 1))
+    assert (n.value > 0) == overflow
+    _lib.check(tracer.lib.mrt_tracer_stack_overflows(tracer._h, C.byref(n), 0))
+    assert n.value == 0
 
 
-def test_tail_counters_alternate_across_launches(tracer):
-    """Back-to-back exporting launches on one stream (the record counter of each is
-    zeroed by the previous one) and a launch with the tail off in between."""
-    bufs, rays, any_hit, want, _ = scene_setup("sponza", 256, 192, "diffuse")
-    saved = tracer.config()
-    try:
-        for cfg in (dict(tail_lanes=64, tail_after_us=1), dict(tail_lanes=-1), dict(tail_lanes=32, tail_after_us=1)):
-            tracer.set_config(**cfg)
-            for _ in range(3):
-                res, _ = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=True)
-                assert np.array_equal(res[:, :2], want[:, :2])
-                if cfg["tail_lanes"] < 0:
-                    assert tracer.last_info["tail_records"] == 0
-    finally:
-        tracer.set_config(**saved)
+def test_oversized_batch_rejected(tracer):
+    """ray/result addressing stays inside int32 — more than 2^30 rays per
+    launch is refused before anything is read (the caller splits the batch)."""
+    from mrt.tracer import GpuBvh
+    tracer.set_bvh(GpuBvh(kat.scene_two_floors()))
+    dummy = torch.zeros(16, dtype=torch.int32, device="cuda")
+    rc = tracer.lib.mrt_tracer_trace(tracer._h, dummy.data_ptr(), dummy.data_ptr(), (1 << 30) + 1, 0, None, None)
+    assert rc == 5   # MRT_ERR_TOO_LARGE
 
 
 def test_invalid_config_rejected(tracer):
@@ -278,9 +299,7 @@ def test_invalid_config_rejected(tracer):
     with pytest.raises(MrtError):
         tracer.set_config(schedule=3)
     with pytest.raises(MrtError):
-        tracer.set_config(tail_lanes=65)
-    with pytest.raises(MrtError):
-        tracer.set_config(tail_resume_lanes=-2)
+        tracer.set_config(lane_groups=3)
 
 
 # ---------------------------------------------------------------- edge cases

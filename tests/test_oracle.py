@@ -155,3 +155,15 @@ def test_builder_output_is_pinned(scene_name, digest):
     import hashlib
     nodes, woop, tri = mrt.Bvh.build(mrt.Scene.synthetic(scene_name, 0, 1)).buffers()
     assert hashlib.sha256(nodes.tobytes() + woop.tobytes() + tri.tobytes()).hexdigest()[:16] == digest
+
+
+def test_comb_stack_depth_known_answer():
+    """kat.scene_comb: 40 pushes trace to the hand answer; 70 exceed the reference's
+    64-entry stack and the oracle flags the overflow (stats[3]) like the kernel does."""
+    for depth, overflow in ((40, 0), (63, 0), (64, 1), (70, 1)):
+        bufs, r, (tid, t) = kat.scene_comb(depth)
+        res, st, _ = O.trace(np.stack([r]), *bufs, stats=True)
+        assert st[0, 3] == overflow, depth
+        if not overflow:
+            assert res[0, 0] == tid and res[0, 1] == kat.f2i(t)
+            assert st[0, 0] == depth   # every inner node fetched once
