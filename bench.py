@@ -10,21 +10,30 @@ HBM. The headline workload (BASELINE.json configs[1]) is Bunny primary rays at
 stand-ins with the published triangle counts (the OBJ assets are absent).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME] [--extra/--no-extra]
+                  [--scaling weak|strong]
 
-For N>1 launch with torch.distributed.run (one rank per GPU, RCCL): rank 0
-builds the SBVH and broadcasts the Compact2 buffers (the BVH is replicated).
-The job is N samples per pixel of the workload's view, sharded by sample:
-rank r traces the rays of sample r (rank 0's are the reference's pixel-centre
-rays; rank r > 0 samples each pixel at the r-th Halton (2,3) point), so every
-rank traces a distinct, equally sized and equally coherent batch (weak
-scaling, no collective in the timed region); time = max over ranks, value =
-rays counted on all ranks / time. After the timed steps the hit results are
-gathered to rank 0 over RCCL point-to-point (timed separately). Rank 0 prints
-one JSON line.
+Multi-GPU (torch.distributed.run, one rank per GPU, RCCL): rank 0 builds the
+SBVH and broadcasts the Compact2 buffers, which stay in HBM (the BVH is
+replicated). Two scalings are measured in every run:
+
+  * strong (BASELINE configs[4]): ONE fixed RayBuffer — hairball
+    diffuse 1920x1080 x 8 spp = 16.6 M rays, generated as the reference's
+    Renderer does in <= 2^21-ray batches (Renderer.cc:46, RayGen.cc:124-142) —
+    cut into contiguous shards, one per rank, each traced in <= 2^21-ray
+    launches with no collective; T_n = max over ranks. T_1 is measured in the
+    same run (rank 0 traces the whole buffer alone), eta(n) = T_1 / (n T_n),
+    with and without the RCCL gather of the {id, t} results to rank 0. Reported
+    as "strong_scaling" in every line; with --scaling strong it is the line's value.
+  * weak (the headline value by default): the N-GPU job is N samples per pixel
+    of the workload's view, rank r tracing sample r (rank 0's are the reference's
+    pixel-centre rays, rank r > 0 the r-th Halton (2,3) point in each pixel).
+
+Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -37,6 +46,8 @@ sys.path.insert(0, os.path.join(REPO, "gpu-ray-tracing_amd"))
 
 METRIC = "Mrays/s (primary/AO/diffuse) at 1/2/4/8 GPUs; achieved HBM GB/s % of peak"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+MALL_BYTES = 256 << 20  # Infinity Cache: a BVH above this streams from HBM
+PROFILE_TAG = "round2"  # committed rocprofv3 summaries this line cites (profiles/<tag>_<workload>_*)
 
 # README numbers (Kepler-class sm_35 build, hardware unstated) — README.md:46-81.
 REFERENCE_MRAYS = {
@@ -77,6 +88,11 @@ WORKLOADS = {
     "hairball-diffuse-1920x1080": ("hairball", 1920, 1080, "diffuse", 1),
 }
 HEADLINE = "bunny-primary-1024x768"
+EXTRA_N1 = ["bunny-primary-640x480", "conference-ao-640x480", "sponza-diffuse-640x480", "sponza-diffuse2-640x480",
+            "hairball-diffuse-640x480", "hairball-diffuse-1920x1080"]
+# Strong-scaling config: scene, frame, samples per pixel, rays per launch.
+STRONG = {"name": "hairball-diffuse-1920x1080x8spp", "scene": "hairball", "w": 1920, "h": 1080, "spp": 8,
+          "max_batch": 1 << 21}
 
 
 def workload_spec(name):
@@ -87,29 +103,43 @@ def workload_spec(name):
     w, h = (int(v) for v in res.split("x"))
     bounces = int(kind[7:]) if kind.startswith("diffuse") and len(kind) > 7 else 1
     return (scene, w, h, kind.rstrip("0123456789"), bounces)
-EXTRA_N1 = ["bunny-primary-640x480", "conference-ao-640x480", "sponza-diffuse-640x480", "sponza-diffuse2-640x480"]
 
 
-# PMC-measured HBM traffic per launch (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in
-# separate passes, tools/profile_round.sh + tools/summarize_prof.py); counters
-# cannot be read inside this timed process, so the committed profile is cited.
-PMC_PROFILES = {w: f"profiles/round1_{w}_pmc_summary.json" for w in
-                ("bunny-primary-1024x768", "bunny-primary-640x480", "conference-ao-640x480", "sponza-diffuse-640x480",
-                 "sponza-diffuse2-640x480", "hairball-diffuse-640x480")}
-
-
-def pmc_traffic(name):
-    path = os.path.join(REPO, PMC_PROFILES.get(name, "-"))
-    if not os.path.exists(path):
-        return None, None
-    with open(path) as f:
-        s = json.load(f)
-    hbm = s.get("hbm_bytes_per_launch")
-    return (int(hbm["total_corrected"]) if hbm else None), PMC_PROFILES[name]
+def pmc_profile(name):
+    """rocprofv3 PMC summary of a workload (FETCH_SIZE / WRITE_SIZE in separate
+    passes, tools/profile_round.sh + tools/summarize_prof.py): counters cannot be
+    read inside this timed process, so the committed profile is cited."""
+    for tag in (PROFILE_TAG, "round1"):
+        path = os.path.join("profiles", f"{tag}_{name}_pmc_summary.json")
+        if os.path.exists(os.path.join(REPO, path)):
+            with open(os.path.join(REPO, path)) as f:
+                s = json.load(f)
+            hbm = s.get("hbm_bytes_per_launch")
+            if hbm:
+                return int(hbm["total_corrected"]), s.get("avg_ns"), path
+    return None, None, None
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_threads():
+    """Host threads for the CPU baseline: the box's CPU share (OMP_NUM_THREADS is set
+    to it on the GPU boxes; os.cpu_count() reports the whole machine there)."""
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", "16"))))
 
 
 # ----------------------------------------------------------------------------- setup
@@ -144,31 +174,86 @@ def barrier(world):
         dist.barrier()
 
 
-def bvh_for(scene_name, world, rank, cache_dir=None):
-    """Rank 0 builds the SBVH (or loads it from cache_dir/<scene>.dat, the
-    reference's bvhcache idea, Renderer.cc:157-217); the Compact2 buffers are
-    broadcast over RCCL."""
-    import mrt
-    scene = mrt.Scene.synthetic(scene_name, 0, 1)
-    t0 = time.perf_counter()
-    if rank == 0:
-        path = os.path.join(cache_dir, f"{scene_name}.dat") if cache_dir else None
-        if path and os.path.exists(path):
-            bvh = mrt.Bvh.load(path)
-        else:
-            bvh = mrt.Bvh.build(scene)
-            if path:
-                os.makedirs(cache_dir, exist_ok=True)
-                bvh.save(path)
-        bufs = bvh.buffers()
-        stats = bvh.stats()
-    else:
-        bufs, stats = None, None
-    build_s = time.perf_counter() - t0
-    if world > 1:
-        from mrt.dist import replicate_buffers
-        bufs = tuple(replicate_buffers(bufs, src=0))
-    return scene, bufs, stats, build_s
+def reduce_over_ranks(x, world, op="max"):
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda" if DIST_BACKEND == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def gather_floats(x, world):
+    """x from every rank, in rank order (on every rank)."""
+    if world == 1:
+        return [x]
+    import torch
+    import torch.distributed as dist
+    dev = "cuda" if DIST_BACKEND == "nccl" else "cpu"
+    out = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(world)]
+    dist.all_gather(out, torch.tensor([x], dtype=torch.float64, device=dev))
+    return [float(t.item()) for t in out]
+
+
+class SceneCache:
+    """Scenes and their Compact2 BVHs, built once per process. Rank 0 builds the
+    SBVH (or loads it from cache_dir: the reference's bvhcache idea,
+    Renderer.cc:157-217, keyed here by the scene and the builder library's bytes
+    so a rebuilt builder never reads a stale file); the buffers are broadcast
+    over RCCL and stay in HBM on every rank."""
+
+    def __init__(self, world, rank, cache_dir=None):
+        self.world, self.rank, self.cache_dir = world, rank, cache_dir
+        self.entries = {}
+        self._builder_key = None
+
+    def builder_key(self):
+        if self._builder_key is None:
+            from mrt import _lib
+            with open(_lib.HOST_LIB_PATH, "rb") as f:
+                self._builder_key = hashlib.sha1(f.read()).hexdigest()[:12]
+        return self._builder_key
+
+    def get(self, scene_name):
+        if scene_name in self.entries:
+            return self.entries[scene_name]
+        import mrt
+        from mrt.tracer import GpuBvh
+        scene = mrt.Scene.synthetic(scene_name, 0, 1)
+        t0 = time.perf_counter()
+        bufs, stats, cached = None, None, False
+        if self.rank == 0:
+            path = (os.path.join(self.cache_dir, f"{scene_name}-{self.builder_key()}.dat")
+                    if self.cache_dir else None)
+            if path and os.path.exists(path):
+                bvh, cached = mrt.Bvh.load(path), True
+            else:
+                bvh = mrt.Bvh.build(scene)
+                if path:
+                    os.makedirs(self.cache_dir, exist_ok=True)
+                    tmp = f"{path}.{os.getpid()}.tmp"
+                    bvh.save(tmp)
+                    os.replace(tmp, path)
+            bufs, stats = bvh.buffers(), bvh.stats()
+            del bvh
+        build_s = time.perf_counter() - t0
+        if self.world > 1:
+            from mrt.dist import replicate_buffers
+            bufs = tuple(replicate_buffers(bufs, src=0))
+        gbvh = GpuBvh(bufs)   # device tensors from RCCL are bound in place; gloo/numpy are uploaded
+        entry = {"scene": scene, "gbvh": gbvh, "stats": stats, "build_s": build_s, "cached": cached,
+                 "host_bufs": bufs if self.rank == 0 and self.world == 1 else None}
+        self.entries[scene_name] = entry
+        return entry
+
+    def host_buffers(self, scene_name):
+        """(nodes, woop, triIndex) as numpy on this rank (for the CPU baseline)."""
+        e = self.get(scene_name)
+        if e["host_bufs"] is not None:
+            return e["host_bufs"]
+        g = e["gbvh"]
+        return g.nodes.cpu().numpy(), g.woop.cpu().numpy(), g.tri_index.cpu().numpy()
 
 
 def halton(i, base):
@@ -186,22 +271,27 @@ def subpixel_sample(rank):
     return (0.5, 0.5) if rank == 0 else (halton(rank, 2), halton(rank, 3))
 
 
+def mrt_seed(bounce):
+    import mrt
+    return mrt.AO_SEED + bounce
+
+
 class Batches:
     """Ray batches of one workload, generated on the device like the reference
     Renderer (Renderer.cc:112-152,242-291; RayGen.cc:50-120): primary rays in
     Morton order; AO/diffuse rays from the traced primary hits (degenerate
-    tmax=-1 rays for misses are traced too; only primary hits are counted)."""
+    tmax=-1 rays for misses are traced too; only primary hits are counted).
+    "diffuseN" chains N bounces, each generated from the previous bounce's hits."""
 
-    def __init__(self, name, scene, bufs, tracer, rank=0):
+    def __init__(self, name, scene, gbvh, tracer, rank=0):
         from mrt.raygen import DeviceRayGen
-        from mrt.tracer import GpuBvh
         sname, w, h, kind, bounces = workload_spec(name)
         self.name, self.kind, self.w, self.h = name, kind, w, h
-        self.gbvh = GpuBvh(bufs)
-        tracer.set_bvh(self.gbvh)
+        tracer.set_bvh(gbvh)
         cam, ao_radius = scene.camera()
         gen = DeviceRayGen(scene)   # RayGen on the device (mrt_raygen_*), like the reference's RayGenKernels
         prim, _ = gen.primary(cam, w, h, subpixel=subpixel_sample(rank))
+        self.primary = prim
         self.batches = []   # (RayBuffer, rays counted)
         if kind == "primary":
             self.batches.append((prim, w * h))
@@ -220,18 +310,13 @@ class Batches:
         self.rays_traced = sum(rb.size for rb, _ in self.batches)
 
 
-def mrt_seed(bounce):
-    import mrt
-    return mrt.AO_SEED + bounce
-
-
 def algorithmic_bytes(tracer, batches):
     """B_ray = 32 + 8 + 64 N_node + 48 N_tri + 16 N_leaf + 4 [hit],
     with the per-ray counts of the single-ray traversal order (the kernel's
     per-lane mode, which reproduces the CPU restatement's counters exactly)."""
     import torch
     total, nodes, tris, leaves = 0, 0, 0, 0
-    for rb, _ in batches.batches:
+    for rb, _ in batches:
         saved = rb.results.clone()
         tracer.trace_batch(rb, exact_rcp=True, speculative=False, stats=True)
         s = rb.stats.to(torch.int64)
@@ -240,50 +325,58 @@ def algorithmic_bytes(tracer, batches):
         nodes, tris, leaves = nodes + n, tris + t, leaves + l
         total += 40 * rb.size + 64 * n + 48 * t + 16 * l + 4 * hits
         rb.results.copy_(saved)
+        rb.stats = None
     return total, nodes, tris, leaves
 
 
-def time_steps(tracer, batches, steps, warmup, world, exact):
-    """Warmup, then exactly `steps` steps bracketed by barrier + synchronize.
-    One HIP event pair on the launch stream around the K steps gives the GPU
-    time per launch (kernel duration plus the inter-launch gap, an upper bound on
-    the kernel's own average); no per-launch host work besides the launch."""
+def warm(launches, warmup, min_seconds=0.3):
+    """At least `warmup` steps and at least min_seconds of back-to-back launches, so
+    the timed steps never run on ramping clocks (a 20-step default on 0.15 ms steps
+    measured 4.8-5.3 G rays/s against 5.35 G once the clocks settle)."""
     import torch
-    stream = torch.cuda.current_stream()
-    launches = [tracer.launcher(rb, exact_rcp=exact, stream=stream) for rb, _ in batches.batches]
-    for _ in range(warmup):
+    t0, done = time.perf_counter(), 0
+    while done < warmup or time.perf_counter() - t0 < min_seconds:
         for go in launches:
             go()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        done += 1
+        if done % 16 == 0:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    return done
+
+
+def time_steps(launches, steps, warmup, world):
+    """Warmup, then exactly `steps` steps bracketed by barrier + synchronize; wall
+    time of the K steps. Then a probe pass on the same stream: every launch
+    bracketed by its own HIP event pair, the mean of which is the kernel's
+    average launch duration (without inter-launch gaps)."""
+    import torch
+    stream = torch.cuda.current_stream()
+    warmed = warm(launches, warmup)
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    e0.record(stream)
     for _ in range(steps):
         for go in launches:
             go()
-    e1.record(stream)
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    launch_ms = e0.elapsed_time(e1) / (steps * len(launches))
-    return wall, launch_ms
-
-
-def reduce_over_ranks(x, world, op="max"):
-    if world == 1:
-        return x
-    import torch
-    import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda" if DIST_BACKEND == "nccl" else "cpu")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
-    return float(t.item())
-
-
-def max_over_ranks(x, world):
-    return reduce_over_ranks(x, world, "max")
+    probe = max(3, min(steps, 50))
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(probe * len(launches))]
+    k = 0
+    for _ in range(probe):
+        for go in launches:
+            ev[k][0].record(stream)
+            go()
+            ev[k][1].record(stream)
+            k += 1
+    torch.cuda.synchronize()
+    per_launch = [a.elapsed_time(b) for a, b in ev]
+    return wall, float(np.mean(per_launch)), warmed
 
 
 def gather_to_root(batches, world):
@@ -303,50 +396,87 @@ def gather_to_root(batches, world):
             nbytes += full.numel() * 4
     torch.cuda.synchronize()
     ms = 1e3 * (time.perf_counter() - t0)
-    return max_over_ranks(ms, world), nbytes
+    return reduce_over_ranks(ms, world), nbytes
 
 
-def cpu_baseline(batches, bufs, threads):
-    """The oracle (oracle/, a scalar C restatement of the same traversal) on the
-    host cores: the first batch of the workload, best of 3 after 1 warmup. Also
-    checks the GPU results of that batch against it (parity on the bench input)."""
+def cpu_baseline(batches, bufs, counted, threads, label):
+    """The oracle (oracle/, a scalar C restatement of the same traversal, one ray at a
+    time, std::thread-style dynamic chunks) on the host cores over every batch of the
+    workload: best of 5 after 1 warmup. Also checks the GPU results against it
+    (parity on the bench input: closest hit bit-identical, any hit hit/miss-identical)."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib as O
-    rb, counted = batches.batches[0]
-    rays = rb.rays.cpu().numpy()
-    any_hit = not rb.need_closest_hit
     nodes, woop, tri = bufs
-    res, _, _ = O.trace(rays, nodes, woop, tri, any_hit=any_hit, threads=threads)
-    best = min(O.trace(rays, nodes, woop, tri, any_hit=any_hit, threads=threads)[2] for _ in range(3))
-    gpu = rb.results_numpy()
-    exact = float(((gpu[:, 0] == res[:, 0]) & (gpu[:, 1] == res[:, 1])).mean())
+    host = [(rb.rays.cpu().numpy(), not rb.need_closest_hit, rb.results_numpy()) for rb, _ in batches]
+    secs, agree, n = [], 0, 0
+    for rep in range(6):
+        total = 0.0
+        for rays, any_hit, gpu in host:
+            res, _, s = O.trace(rays, nodes, woop, tri, any_hit=any_hit, threads=threads)
+            total += s
+            if rep == 0:
+                same = (gpu[:, 0] == -1) == (res[:, 0] == -1) if any_hit else \
+                    (gpu[:, 0] == res[:, 0]) & (gpu[:, 1] == res[:, 1])
+                agree += int(same.sum())
+                n += len(rays)
+        if rep:
+            secs.append(total)
+    best = min(secs)
+    rays = sum(len(r) for r, _, _ in host)
     return {"value": round(counted / best / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{batches.name} batch 0: {rb.size} rays ({counted} counted), best of 3 after 1 warmup, "
-                      f"{threads} threads, oracle/trace_oracle.c",
-            "parity_exact_fraction": exact}
+            "cpu_model": cpu_model(), "seconds_best": round(best, 4),
+            "sample": f"{label}: all {len(host)} batch(es), {rays} rays ({counted} counted), best of 5 after 1 "
+                      f"warmup, {threads} threads, oracle/trace_oracle.c (same Compact2 bytes, same rays)",
+            "parity_exact_fraction": round(agree / max(1, n), 6)}
 
 
-def run_workload(name, tracer, world, rank, steps, warmup, exact, want_cpu, cache_dir=None):
+def roofline(name, alg_bytes_per_launch, kernel_ms, bvh_bytes):
+    """achieved = algorithmic bytes per launch / average kernel
+    duration; traffic = PMC-measured HBM bytes per launch (committed rocprofv3
+    summary) and the HBM rate they imply. bound: the BVH of a cache-resident scene
+    never leaves the 256 MB MALL/L2 (algorithmic GB/s can then exceed the HBM
+    peak), so the kernel is latency-bound; only a BVH above the MALL streams from HBM,
+    and even there the measured traffic rate is what the HBM fraction is."""
+    traffic, prof_ns, src = pmc_profile(name)
+    achieved = alg_bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+    out = {"bound": "latency", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+           "algorithmic_bytes_per_launch": int(alg_bytes_per_launch), "kernel_ms": round(kernel_ms, 4),
+           "bvh_bytes": int(bvh_bytes), "bvh_exceeds_mall": bvh_bytes > MALL_BYTES}
+    if traffic:
+        hbm = traffic / (kernel_ms * 1e-3) / 1e9
+        out.update({"hbm_measured_GBps": round(hbm, 1), "hbm_measured_frac": round(hbm / HBM_PEAK_GBS, 4),
+                    "traffic_source": src,
+                    "profile_kernel_ms": round(prof_ns / 1e6, 4) if prof_ns else None})
+        if hbm > 0.5 * HBM_PEAK_GBS:
+            out["bound"] = "hbm"
+    out["bound_basis"] = ("measured HBM traffic near peak" if out["bound"] == "hbm" else
+                          "dependent node->node fetch chains; measured HBM rate well below peak"
+                          if traffic else "cache-resident BVH; dependent fetch chains (no PMC profile cited)")
+    return out
+
+
+def run_workload(name, tracer, scenes, world, rank, steps, warmup, exact, want_cpu):
     scene_name = workload_spec(name)[0]
-    scene, bufs, bstats, build_s = bvh_for(scene_name, world, rank, cache_dir)
-    batches = Batches(name, scene, bufs, tracer, rank)
-    alg_bytes, n_nodes, n_tris, n_leaves = algorithmic_bytes(tracer, batches)
-    wall, launch_ms = time_steps(tracer, batches, steps, warmup, world, exact)
-    wall = max_over_ranks(wall, world)
-    launch_ms = max_over_ranks(launch_ms, world)
+    e = scenes.get(scene_name)
+    batches = Batches(name, e["scene"], e["gbvh"], tracer, rank)
+    alg_bytes, n_nodes, n_tris, n_leaves = algorithmic_bytes(tracer, batches.batches)
+    launches = [tracer.launcher(rb, exact_rcp=exact) for rb, _ in batches.batches]
+    wall, launch_ms, warmed = time_steps(launches, steps, warmup, world)
+    wall = reduce_over_ranks(wall, world)
+    launch_ms = reduce_over_ranks(launch_ms, world)
     counted = int(reduce_over_ranks(batches.rays_counted, world, "sum"))
     traced = int(reduce_over_ranks(batches.rays_traced, world, "sum"))
-    alg_bytes = reduce_over_ranks(alg_bytes, world, "sum") / world   # per-GPU launch bytes (mean over ranks)
-    ms_per_step = 1e3 * wall / steps
+    alg_bytes = reduce_over_ranks(alg_bytes, world, "sum") / world   # per-GPU bytes (mean over ranks)
     value = counted * steps / wall / 1e6
     gather = gather_to_root(batches, world) if world > 1 else None
-    kernel_ms_per_step = launch_ms * len(batches.batches)
-    achieved = alg_bytes / (kernel_ms_per_step * 1e-3) / 1e9
+    g = e["gbvh"]
     out = {
         "workload": name,
         "value": round(value, 2),
-        "ms_per_step": round(ms_per_step, 4),
+        "ms_per_step": round(1e3 * wall / steps, 4),
         "kernel_ms_per_launch": round(launch_ms, 4),
+        "warmup_steps_run": warmed,
         "rays_counted": batches.rays_counted,
         "rays_traced": batches.rays_traced,
         "mrays_traced_per_s": round(traced * steps / wall / 1e6, 2),
@@ -354,48 +484,112 @@ def run_workload(name, tracer, world, rank, steps, warmup, exact, want_cpu, cach
         "gather": ({"ms": round(gather[0], 3), "bytes_to_root": gather[1],
                     "value_incl_gather": round(counted * steps / (wall + steps * gather[0] / 1e3) / 1e6, 2)}
                    if gather else None),
-        "scene_tris": scene.num_triangles,
-        "bvh": {"inner_nodes": len(bufs[0]) // 16, "woop_slots": len(bufs[1]) // 4,
-                "bytes": 4 * (len(bufs[0]) + len(bufs[1]) + len(bufs[2])), "build_s": round(build_s, 2),
-                **({"max_depth": bstats["max_depth"], "sah": round(bstats["sah_cost"], 2)} if bstats else {})},
+        "scene_tris": e["scene"].num_triangles,
+        "bvh": {"inner_nodes": g.nodes.numel() // 16, "woop_slots": g.woop.numel() // 4, "bytes": g.total_bytes,
+                "build_s": round(e["build_s"], 2), "from_cache": e["cached"],
+                **({"max_depth": e["stats"]["max_depth"], "sah": round(e["stats"]["sah_cost"], 2)}
+                   if e["stats"] else {})},
         "per_ray": {"nodes": round(n_nodes / batches.rays_traced, 2), "tris": round(n_tris / batches.rays_traced, 2),
                     "leaves": round(n_leaves / batches.rays_traced, 2),
                     "bytes": round(alg_bytes / batches.rays_traced, 1)},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(name)[0],
-                     "traffic_source": pmc_traffic(name)[1],
-                     "algorithmic_bytes_per_launch": int(alg_bytes / len(batches.batches))},
+        "roofline": roofline(name, alg_bytes / len(batches.batches), launch_ms, g.total_bytes),
         "reference_mrays": REFERENCE_MRAYS.get(name),
     }
     if want_cpu:
-        out["cpu_baseline"] = cpu_baseline(batches, bufs, threads=min(16, os.cpu_count() or 1))
+        out["cpu_baseline"] = cpu_baseline(batches.batches, scenes.host_buffers(scene_name), batches.rays_counted,
+                                           host_threads(), name)
     return out
+
+
+def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact):
+    """one fixed RayBuffer (the hairball diffuse frame at 8 spp,
+    generated by the Renderer's <= 2^21-ray batches with their glibc seeds), cut
+    into contiguous shards; every rank traces its shard in <= 2^21-ray launches.
+    T_n = max over ranks; T_1 = rank 0 tracing the whole buffer alone, same run;
+    then the {id, t} gather to rank 0, checked against the single-GPU results."""
+    import torch
+    from mrt.dist import gather_results, shard_launches, shard_range, trace_shard
+    from mrt.raygen import RAY_DIFFUSE
+    from mrt.renderer import Renderer
+    from mrt.tracer import RayBuffer
+    cfg = STRONG
+    e = scenes.get(cfg["scene"])
+    tracer.set_bvh(e["gbvh"])
+    cam, _ = e["scene"].camera()
+    r = Renderer(tracer, e["scene"], max_batch=cfg["max_batch"], exact_rcp=True)
+    r.set_params(RAY_DIFFUSE, cfg["spp"])
+    r.begin_frame(cam, cfg["w"], cfg["h"])
+    counted = r.total_num_rays()
+    parts = [b for b, _ in r.batches()]
+    n = sum(b.size for b in parts)
+    big = RayBuffer(torch.cat([b.rays for b in parts]), need_closest_hit=True)
+    del parts, r
+    torch.cuda.synchronize()
+    lo, hi = shard_range(n, world, rank)
+    launches = [tracer.launcher(big.view(a, b), exact_rcp=exact) for a, b in shard_launches(lo, hi, cfg["max_batch"])]
+    wall, launch_ms, _ = time_steps(launches, steps, warmup, world)
+    per_rank = gather_floats(wall / steps * 1e3, world)
+    tn = max(per_rank)
+    # gather of this shard's {id, t} to rank 0 (RCCL point-to-point; gloo: via host)
+    torch.cuda.synchronize()
+    barrier(world)
+    t0 = time.perf_counter()
+    res = big.results[lo:hi] if DIST_BACKEND == "nccl" else big.results[lo:hi].cpu()
+    full = gather_results(res, n) if world > 1 else big.results[:, :2]
+    torch.cuda.synchronize()
+    gather_ms = reduce_over_ranks(1e3 * (time.perf_counter() - t0), world) if world > 1 else 0.0
+    # T_1 in the same run: rank 0 alone over the whole buffer (the others wait)
+    if world > 1:
+        equal = None
+        if rank == 0:
+            one = [tracer.launcher(big.view(a, b), exact_rcp=exact) for a, b in shard_launches(0, n, cfg["max_batch"])]
+            w1, _, _ = time_steps(one, steps, warmup, 1)
+            t1 = w1 / steps * 1e3
+            equal = bool(torch.equal(full.to(big.results.device), big.results[:, :2]))
+        barrier(world)
+        t1 = reduce_over_ranks(t1 if rank == 0 else 0.0, world)
+    else:
+        t1, equal = tn, True
+    return {
+        "workload": cfg["name"], "rays_traced": n, "rays_counted": counted, "launch_rays_max": cfg["max_batch"],
+        "shard_rays": hi - lo, "n_gpus": world, "t1_ms": round(t1, 4), "tn_ms": round(tn, 4),
+        "per_rank_ms": [round(x, 4) for x in per_rank], "kernel_ms_per_launch": round(launch_ms, 4),
+        "eta": round(t1 / (world * tn), 4), "gather_ms": round(gather_ms, 3),
+        "eta_with_gather": round(t1 / (world * (tn + gather_ms)), 4),
+        "value": round(counted / (tn * 1e-3) / 1e6, 2), "value_with_gather": round(counted / ((tn + gather_ms) * 1e-3) / 1e6, 2),
+        "gathered_equals_single_gpu": equal,
+        "collective": f"{DIST_BACKEND} point-to-point gather of {n * 8} B to rank 0" if world > 1 else None,
+    }
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)   # 0.15 ms steps: 20 left clocks ramping (4.8-5.3 G vs 5.35 G stable)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20, help="minimum warmup steps (warmup also runs >= 0.3 s)")
     ap.add_argument("--workload", default=HEADLINE, help="a WORKLOADS key or <scene>-<ray>-<W>x<H>")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="which measurement is the line's value (both are reported)")
     ap.add_argument("--rcp", default="exact", choices=["exact", "fast"],
                     help="exact = correctly rounded 1/x (bit-identical to the oracle); fast = v_rcp_f32")
     ap.add_argument("--extra", dest="extra", action="store_true", default=None,
-                    help="also measure the AO/diffuse configs (default on at N=1)")
+                    help="also measure the AO/diffuse/hairball configs (default on at N=1)")
     ap.add_argument("--no-extra", dest="extra", action="store_false")
+    ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling measurement")
+    ap.add_argument("--strong-steps", type=int, default=10)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--waves-per-cu", type=int, default=0)
     ap.add_argument("--fetch-threshold", type=int, default=-1)
     ap.add_argument("--lds-stack", type=int, default=0)
     ap.add_argument("--queues", type=int, default=0)
     ap.add_argument("--schedule", type=int, default=0, help="1 while-while, 2 if-if (0: library default)")
-    ap.add_argument("--bvh-cache", default=None, help="directory of <scene>.dat Compact2 caches (built if missing)")
+    ap.add_argument("--bvh-cache", default=os.path.join(os.environ.get("TMPDIR", "/tmp"), "mrt_bvhcache"),
+                    help="directory of Compact2 .dat caches (built if missing); '' disables")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (RCCL) for real runs; gloo only to rehearse N>1 ranks on one GPU")
     ap.add_argument("--lane-groups", type=int, default=0)
     args = ap.parse_args()
 
-    import torch
     from mrt.tracer import Tracer
 
     rank, world, local = dist_setup(args.gpus, args.dist_backend)
@@ -417,46 +611,64 @@ def main():
         tracer.set_config(**cfg)
     exact = args.rcp == "exact"
     want_cpu = (rank == 0 and world == 1 and not args.no_cpu)
+    scenes = SceneCache(world, rank, args.bvh_cache or None)
 
-    head = run_workload(args.workload, tracer, world, rank, args.steps, args.warmup, exact, want_cpu, args.bvh_cache)
+    head = run_workload(args.workload, tracer, scenes, world, rank, args.steps, args.warmup, exact, want_cpu)
+    log(f"[head] {args.workload}: {head['value']} Mrays/s")
     extras = []
     do_extra = args.extra if args.extra is not None else (world == 1)
     if do_extra:
         for name in EXTRA_N1:
             if name != args.workload:
-                r = run_workload(name, tracer, world, rank, args.steps, args.warmup, exact, False, args.bvh_cache)
+                r = run_workload(name, tracer, scenes, world, rank, args.steps, args.warmup, exact, want_cpu)
                 extras.append(r)
-                log(f"[extra] {name}: {r['value']} Mrays/s (reference {r['reference_mrays']})")
+                log(f"[extra] {name}: {r['value']} Mrays/s (reference {r['reference_mrays']}, "
+                    f"cpu {r.get('cpu_baseline', {}).get('value')})")
+    strong = None
+    if not args.no_strong or args.scaling == "strong":
+        strong = strong_scaling(tracer, scenes, world, rank, args.strong_steps, 3, exact)
+        log(f"[strong] {strong['workload']} n={world}: T1 {strong['t1_ms']} ms, Tn {strong['tn_ms']} ms, "
+            f"eta {strong['eta']} (with gather {strong['eta_with_gather']})")
 
     if rank == 0:
         ref = REFERENCE_MRAYS.get(args.workload)
+        spec = workload_spec(args.workload)
+        if args.scaling == "strong":
+            value, ms_step = strong["value"], strong["tn_ms"]
+            config = {"workload": strong["workload"], "scene": STRONG["scene"], "width": STRONG["w"],
+                      "height": STRONG["h"], "samples_per_pixel": STRONG["spp"], "rays_total": strong["rays_traced"],
+                      "rcp": args.rcp, "parallelism": f"one RayBuffer in {world} contiguous shards, BVH replicated",
+                      "tracer": tracer.config()}
+        else:
+            value, ms_step = head["value"], head["ms_per_step"]
+            config = {"workload": args.workload, "scene": spec[0], "scene_tris": head["scene_tris"], "width": spec[1],
+                      "height": spec[2], "ray_type": spec[3], "rays_per_gpu": head["rays_counted"], "rcp": args.rcp,
+                      "parallelism": (f"rays sharded by pixel sample x{world}, BVH replicated "
+                                      f"(weak: one {spec[1]}x{spec[2]} sample per GPU, no collective in the step)"),
+                      "tracer": tracer.config()}
         line = {
             "metric": METRIC,
-            "value": head["value"],
+            "value": value,
             "unit": "Mrays/s",
             "n_gpus": world,
-            "steps": args.steps,
+            "steps": args.steps if args.scaling == "weak" else args.strong_steps,
             "warmup": args.warmup,
-            "ms_per_step": head["ms_per_step"],
+            "ms_per_step": ms_step,
             "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": round(head["value"] / ref, 3) if ref else None,
+            "scaling": args.scaling,
+            "vs_baseline": round(head["value"] / ref, 3) if (ref and args.scaling == "weak") else None,
             "dtype": "f32",
             "data": "synthetic (deterministic stand-in scene with the README triangle count; rays generated on the device)",
-            "config": {"workload": args.workload, "scene": workload_spec(args.workload)[0],
-                       "scene_tris": head["scene_tris"], "width": workload_spec(args.workload)[1],
-                       "height": workload_spec(args.workload)[2], "ray_type": workload_spec(args.workload)[3],
-                       "rays_per_gpu": head["rays_counted"], "rcp": args.rcp,
-                       "parallelism": (f"rays sharded by pixel sample x{world}, BVH replicated "
-                                       f"(weak: one {workload_spec(args.workload)[1]}x{workload_spec(args.workload)[2]} "
-                                       f"sample per GPU, no collective in the step)"),
-                       "tracer": tracer.config()},
-            "roofline": head["roofline"],
+            "config": config,
+            "roofline": head["roofline"] if args.scaling == "weak" else None,
             "cpu_baseline": head.get("cpu_baseline"),
+            "strong_scaling": strong,
             "detail": {k: head[k] for k in ("kernel_ms_per_launch", "rays_traced", "mrays_traced_per_s", "bvh",
-                                            "per_ray", "reference_mrays", "rays_counted_all_ranks", "gather")},
-            "extra_workloads": [{k: r[k] for k in ("workload", "value", "reference_mrays", "kernel_ms_per_launch",
-                                                   "rays_counted", "rays_traced", "per_ray", "roofline", "bvh")}
+                                            "per_ray", "reference_mrays", "rays_counted_all_ranks", "gather",
+                                            "warmup_steps_run")},
+            "extra_workloads": [{k: r.get(k) for k in ("workload", "value", "reference_mrays", "kernel_ms_per_launch",
+                                                       "rays_counted", "rays_traced", "per_ray", "roofline", "bvh",
+                                                       "cpu_baseline")}
                                 for r in extras],
         }
         print(json.dumps(line), flush=True)

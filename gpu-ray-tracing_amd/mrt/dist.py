@@ -21,8 +21,10 @@ def shard_range(n: int, world: int, rank: int) -> tuple[int, int]:
 
 
 def replicate_buffers(bufs, src: int = 0, device=None):
-    """Broadcast int32 numpy buffers (e.g. Compact2 nodes/woop/triIndex) from
-    rank `src`; other ranks pass None. Returns numpy copies on every rank."""
+    """Broadcast int32 buffers (e.g. Compact2 nodes/woop/triIndex) from rank `src`;
+    other ranks pass None. Returns tensors on `device` on every rank: with RCCL
+    they stay in HBM (the BVH crosses xGMI once and is bound in place, GpuBvh
+    accepts them without a copy); with gloo they are CPU tensors."""
     rank = dist.get_rank()
     dev = device if device is not None else (torch.device("cuda", torch.cuda.current_device())
                                              if dist.get_backend() == "nccl" else torch.device("cpu"))
@@ -35,12 +37,31 @@ def replicate_buffers(bufs, src: int = 0, device=None):
     out = []
     for i in range(count):
         if rank == src:
-            t = torch.from_numpy(np.ascontiguousarray(bufs[i], np.int32)).to(dev)
+            b = bufs[i]
+            t = (b.to(dev, torch.int32) if isinstance(b, torch.Tensor)
+                 else torch.from_numpy(np.ascontiguousarray(b, np.int32)).to(dev))
         else:
             t = torch.empty(int(sizes[i]), dtype=torch.int32, device=dev)
         dist.broadcast(t, src)
-        out.append(t.cpu().numpy())
+        out.append(t)
     return out
+
+
+def shard_launches(lo: int, hi: int, max_rays: int):
+    """The shard [lo, hi) cut into launches of at most max_rays rays (the reference
+    traces at most 2^21 rays per launch, Renderer.cc:46)."""
+    return [(a, min(hi, a + max_rays)) for a in range(lo, hi, max_rays)]
+
+
+def trace_shard(tracer, rays, world: int, rank: int, max_rays: int = 1 << 21, exact_rcp: bool = True,
+                stream=None):
+    """Strong-scaling step of one rank: trace its contiguous shard of the RayBuffer
+    `rays` (every rank holds the same buffer) in launches of at most max_rays rays,
+    stream-ordered, results written in place. Returns the shard's (lo, hi)."""
+    lo, hi = shard_range(rays.size, world, rank)
+    for a, b in shard_launches(lo, hi, max_rays):
+        tracer.trace_async(rays.view(a, b), exact_rcp=exact_rcp, stream=stream)
+    return lo, hi
 
 
 def gather_results(local: torch.Tensor, n_total: int, dst: int = 0):

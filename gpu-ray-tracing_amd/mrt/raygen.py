@@ -60,16 +60,21 @@ class DeviceRayGen:
         return RayBuffer(rays, need_closest_hit=True, device=self.device), slot_to_id
 
     def ao(self, rays: RayBuffer, num_samples: int, max_dist: float, seed: int = AO_SEED, closest_hit: bool = False,
-           stream=None) -> RayBuffer:
+           stream=None, first: int = 0, count: int | None = None) -> RayBuffer:
         """RayGen::ao over a traced batch: num_samples hemisphere rays per input ray
-        (any-hit for AO; closest_hit=True with max_dist=far is the diffuse bounce)."""
+        (any-hit for AO; closest_hit=True with max_dist=far is the diffuse bounce).
+        first/count select the input rays [first, first + count) — one batch of
+        RayGen::batching (RayGen.cc:77-120: firstInputSlot, numInputRays); the
+        rotation hash and the output slots count from the batch's first ray."""
         if self.normals is None:
             raise _lib.MrtError("DeviceRayGen.ao needs the scene's triangle normals (pass scene=)")
-        n = rays.size
+        n = rays.size - first if count is None else count
+        if first < 0 or n < 0 or first + n > rays.size:
+            raise _lib.MrtError(f"input range [{first}, {first + n}) outside the {rays.size}-ray batch")
         out = torch.empty((n * num_samples, 8), dtype=torch.float32, device=self.device)
-        _lib.check(self.lib.mrt_raygen_ao(rays.rays.data_ptr(), rays.results.data_ptr(), n, self.normals.data_ptr(),
-                                          self.num_tris, num_samples, float(max_dist), seed & 0xFFFFFFFF,
-                                          out.data_ptr(), None, None, _stream_ptr(stream)))
+        _lib.check(self.lib.mrt_raygen_ao(rays.rays.data_ptr() + 32 * first, rays.results.data_ptr() + 16 * first, n,
+                                          self.normals.data_ptr(), self.num_tris, num_samples, float(max_dist),
+                                          seed & 0xFFFFFFFF, out.data_ptr(), None, None, _stream_ptr(stream)))
         return RayBuffer(out, need_closest_hit=closest_hit, device=self.device)
 
     def count_hits_async(self, rays: RayBuffer, stream=None) -> torch.Tensor:
@@ -98,22 +103,27 @@ class DeviceReconstructor:
 
     def reconstruct(self, ray_type: int, primary: RayBuffer, slot_to_id: torch.Tensor, num_pixels: int,
                     batch: RayBuffer | None = None, num_samples: int = 1, pixels: torch.Tensor | None = None,
-                    batch_id_to_slot: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+                    batch_id_to_slot: torch.Tensor | None = None, stream=None, first_primary: int = 0) -> torch.Tensor:
         """num_pixels int32 (ABGR bits) pixels; batch defaults to the primary batch.
-        AO/diffuse batches hold num_samples rays per primary ray (mrt_raygen_ao's layout)."""
+        AO/diffuse batches hold num_samples rays per primary ray (mrt_raygen_ao's layout);
+        a batch of RayGen::batching covers the primaries [first_primary, first_primary +
+        batch.size / num_samples) (Renderer::updateResult, Renderer.cc:421-445)."""
         if batch is None:
             batch = primary
-        n_primary = primary.size
-        if ray_type == RAY_PRIMARY and (num_samples != 1 or batch.size != n_primary):
+        if ray_type == RAY_PRIMARY and (num_samples != 1 or batch.size != primary.size or first_primary):
             raise _lib.MrtError("primary reconstruction takes the primary batch with one ray per pixel")
-        if ray_type != RAY_PRIMARY and batch.size != n_primary * num_samples:
-            raise _lib.MrtError(f"batch holds {batch.size} rays, expected {n_primary} x {num_samples}")
-        if slot_to_id.numel() != n_primary:
+        if batch.size % num_samples:
+            raise _lib.MrtError(f"batch holds {batch.size} rays, not a multiple of {num_samples}")
+        n_primary = batch.size // num_samples
+        if first_primary < 0 or first_primary + n_primary > primary.size:
+            raise _lib.MrtError(f"batch covers primaries [{first_primary}, {first_primary + n_primary}) "
+                                f"outside the {primary.size}-ray primary batch")
+        if slot_to_id.numel() != primary.size:
             raise _lib.MrtError("slot_to_id must hold one pixel id per primary ray")
         if pixels is None:
             pixels = torch.zeros(num_pixels, dtype=torch.int32, device=self.device)
         b2s = None if batch_id_to_slot is None else batch_id_to_slot.data_ptr()
-        _lib.check(self.lib.mrt_reconstruct(ray_type, num_samples, 0, n_primary, slot_to_id.data_ptr(),
+        _lib.check(self.lib.mrt_reconstruct(ray_type, num_samples, first_primary, n_primary, slot_to_id.data_ptr(),
                                             primary.results.data_ptr(), b2s, batch.results.data_ptr(),
                                             self.material.data_ptr(), self.shaded.data_ptr(), pixels.data_ptr(),
                                             _stream_ptr(stream)))

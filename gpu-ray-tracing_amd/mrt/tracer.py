@@ -29,11 +29,16 @@ class GpuBvh:
     """Compact2 node / Woop / triIndex buffers uploaded to the current device."""
 
     def __init__(self, bvh: Bvh | tuple, device=None):
+        """bvh: a host Bvh, or (nodes, woop, triIndex) as int32 numpy arrays or tensors
+        (device tensors, e.g. from mrt.dist.replicate_buffers, are bound in place)."""
         nodes, woop, tri = bvh.buffers() if isinstance(bvh, Bvh) else bvh
         dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-        self.nodes = torch.from_numpy(np.ascontiguousarray(nodes, np.int32)).to(dev)
-        self.woop = torch.from_numpy(np.ascontiguousarray(woop, np.int32)).to(dev)
-        self.tri_index = torch.from_numpy(np.ascontiguousarray(tri, np.int32)).to(dev)
+
+        def upload(a):
+            if isinstance(a, torch.Tensor):
+                return a.to(dev, torch.int32).contiguous()
+            return torch.from_numpy(np.ascontiguousarray(a, np.int32)).to(dev)
+        self.nodes, self.woop, self.tri_index = upload(nodes), upload(woop), upload(tri)
         self.device = dev
 
     @property
@@ -59,15 +64,26 @@ class RayBuffer:
     needClosestHit selects the trace mode exactly like the reference
     (anyHit = !needClosestHit, CudaTracer.cc:172)."""
 
-    def __init__(self, rays, need_closest_hit: bool = True, device=None):
+    def __init__(self, rays, need_closest_hit: bool = True, device=None, results: torch.Tensor | None = None):
+        """results: an existing int32 [n, 4] device tensor to write into (e.g. a
+        slice of a larger RayResult array, for the shards of one RayBuffer)."""
         dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         if isinstance(rays, torch.Tensor):
             self.rays = rays.to(dev, torch.float32).contiguous().view(-1, 8)
         else:
             self.rays = torch.from_numpy(np.ascontiguousarray(rays, np.float32).reshape(-1, 8)).to(dev)
-        self.results = torch.zeros((self.rays.shape[0], 4), dtype=torch.int32, device=dev)
+        if results is None:
+            results = torch.zeros((self.rays.shape[0], 4), dtype=torch.int32, device=dev)
+        elif tuple(results.shape) != (self.rays.shape[0], 4) or not results.is_contiguous() or \
+                results.dtype != torch.int32:
+            raise ValueError("results must be a contiguous int32 [n, 4] tensor matching the rays")
+        self.results = results
         self.need_closest_hit = need_closest_hit
         self.stats = None
+
+    def view(self, lo: int, hi: int) -> "RayBuffer":
+        """Rays [lo, hi) of this buffer as a RayBuffer sharing its rays and results."""
+        return RayBuffer(self.rays[lo:hi], self.need_closest_hit, self.rays.device, self.results[lo:hi])
 
     @property
     def size(self) -> int:

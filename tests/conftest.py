@@ -5,7 +5,7 @@ import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "gpu-ray-tracing_amd")
-for p in (PKG, os.path.dirname(os.path.abspath(__file__))):
+for p in (PKG, os.path.dirname(os.path.abspath(__file__)), os.path.join(REPO, "oracle")):
     if p not in sys.path:
         sys.path.insert(0, p)
 

@@ -1,7 +1,9 @@
-"""World-size-2 rehearsal of the multi-GPU path on CPU with gloo: the BVH is
+"""World-size-2/3 rehearsal of the multi-GPU path with gloo: the BVH is
 replicated from rank 0, rays are sharded contiguously, each rank traces its
-shard (here with the CPU oracle standing in for the per-GPU tracer), and the
-results are gathered to rank 0 in ray order."""
+shard, and the results are gathered to rank 0 in ray order. On CPU the oracle
+stands in for the per-GPU tracer; the GPU test runs two ranks on one MI355X
+through the real HIP tracer (mrt.dist.trace_shard, the bench's strong-scaling
+step) and gathers with gather_results."""
 import os
 import socket
 
@@ -34,7 +36,7 @@ def _worker(rank, world, port, out_path):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     scene = mrt.Scene.synthetic("mori", 0, 1)
     bufs = mrt.Bvh.build(scene).buffers() if rank == 0 else None
-    nodes, woop, tri = replicate_buffers(bufs, src=0, device=torch.device("cpu"))
+    nodes, woop, tri = (t.numpy() for t in replicate_buffers(bufs, src=0, device=torch.device("cpu")))
     cam, _ = scene.camera()
     rays, _ = mrt.primary_rays(cam, 61, 37)          # ragged: 2257 rays, not a multiple of the world size
     lo, hi = shard_range(len(rays), world, rank)
@@ -62,3 +64,55 @@ def test_shard_ranges_partition():
             assert spans[0][0] == 0 and spans[-1][1] == n
             assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
             assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+
+
+def _gpu_worker(rank, world, port, out_path):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "gpu-ray-tracing_amd"))
+    import mrt
+    from mrt.dist import gather_results, replicate_buffers, trace_shard
+    from mrt.raygen import DeviceRayGen
+    from mrt.tracer import GpuBvh, Tracer
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    scene = mrt.Scene.synthetic("hairball", 800, 1)
+    bufs = mrt.Bvh.build(scene).buffers() if rank == 0 else None
+    rep = replicate_buffers(bufs, src=0, device=torch.device("cpu"))
+    tracer = Tracer(0)
+    tracer.set_bvh(GpuBvh(tuple(rep)))
+    cam, _ = scene.camera()
+    gen = DeviceRayGen(scene)
+    prim, _ = gen.primary(cam, 173, 91)
+    tracer.trace_batch(prim, exact_rcp=True)
+    rays = gen.ao(prim, 3, cam.far, closest_hit=True)   # one fixed RayBuffer, identical on every rank
+    lo, hi = trace_shard(tracer, rays, world, rank, max_rays=4096)   # several launches per shard
+    torch.cuda.synchronize()
+    full = gather_results(rays.results[lo:hi].cpu(), rays.size, dst=0)
+    if rank == 0:
+        np.save(out_path + ".rays.npy", rays.rays.cpu().numpy())
+        np.save(out_path + ".res.npy", full.numpy())
+        for name, b in zip(("nodes", "woop", "tri"), rep):
+            np.save(out_path + f".{name}.npy", b.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_ranks_on_one_gpu_trace_shards_and_gather(tmp_path):
+    """Two gloo ranks sharing one MI355X: replicate -> shard (strong scaling: one fixed
+    RayBuffer, contiguous shards, <= 4096-ray launches) -> HIP trace -> gather to rank 0;
+    the gathered {id, t} equal the oracle over the whole buffer."""
+    import oracle_lib as O
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    out = str(tmp_path / "g")
+    mp.spawn(_gpu_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    rays = np.load(out + ".rays.npy")
+    got = np.load(out + ".res.npy")
+    bufs = tuple(np.load(out + f".{n}.npy") for n in ("nodes", "woop", "tri"))
+    want, _, _ = O.trace(rays, *bufs, threads=8)
+    assert len(got) == len(rays) == 173 * 91 * 3
+    assert np.array_equal(got, want[:, :2])
