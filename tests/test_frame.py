@@ -197,8 +197,12 @@ def test_device_primary_frame_end_to_end(frame, tmp_path):
 def test_device_reconstruct_rejects_bad_shapes(frame):
     scene, cam, ao, bufs, t, g, rec = frame
     prim, s2i = g.primary(cam, 8, 8)
-    with pytest.raises(mrt._lib.MrtError):
-        rec.reconstruct(1, prim, s2i, 64, batch=prim, num_samples=4)
+    with pytest.raises(mrt._lib.MrtError):   # 64 rays are not whole 3-sample groups
+        rec.reconstruct(1, prim, s2i, 64, batch=prim, num_samples=3)
+    with pytest.raises(mrt._lib.MrtError):   # 16 primaries from primary 60 run past the 64-ray primary batch
+        rec.reconstruct(1, prim, s2i, 64, batch=prim, num_samples=4, first_primary=60)
+    with pytest.raises(mrt._lib.MrtError):   # primary reconstruction takes the whole primary batch
+        rec.reconstruct(0, prim, s2i, 64, batch=prim, first_primary=1)
 
 
 def test_reconstruct_argument_checks_without_gpu():
