@@ -20,8 +20,9 @@ def main():
     if len(sys.argv) > 2:
         import json
         tr.set_config(**json.loads(sys.argv[2]))
-    scene, bufs, _, _ = bench.bvh_for(bench.workload_spec(wl)[0], 1, 0)
-    b = bench.Batches(wl, scene, bufs, tr)
+    scenes = bench.SceneCache(1, 0, os.path.join(os.environ.get("TMPDIR", "/tmp"), "mrt_bvhcache"))
+    e = scenes.get(bench.workload_spec(wl)[0])
+    b = bench.Batches(wl, e["scene"], e["gbvh"], tr)
     rb = b.batches[0][0]
     for _ in range(3):
         tr.trace_batch(rb, exact_rcp=True)
@@ -38,10 +39,12 @@ def main():
           f"last end {end.max():.1f} us", flush=True)
     for q in (50, 90, 99, 99.9, 100):
         print(f"  {q:5}% of rays done by {np.percentile(end, q):7.1f} us", flush=True)
-    for lo, hi in ((0, 20), (20, 40), (40, 60), (60, 80), (80, 100), (100, 120), (120, 160), (160, 400)):
+    span = end.max()
+    edges = np.linspace(0, span * 1.0001, 11)
+    for lo, hi in zip(edges[:-1], edges[1:]):
         sel = (end >= lo) & (end < hi)
         if sel.any():
-            print(f"  ending in [{lo},{hi}) us: {sel.sum():7d} rays, start median {np.median(start[sel]):6.1f} "
+            print(f"  ending in [{lo:.0f},{hi:.0f}) us: {sel.sum():7d} rays, start median {np.median(start[sel]):6.1f} "
                   f"dur median {np.median(dur[sel]):6.1f} max {dur[sel].max():6.1f} steps median {np.median(steps[sel]):5.0f} "
                   f"max {steps[sel].max()}", flush=True)
     order = np.argsort(end)[::-1]
@@ -54,7 +57,7 @@ def main():
     print("  last-finishing waves (end us, rays, first starts):")
     for w, v in sorted(wend.items(), key=lambda kv: -kv[1][0])[:10]:
         print(f"    wave {w}: end {v[0]:.1f} rays {v[1]} starts {v[2]}")
-    bins = np.arange(0, end.max() + 5, 5.0)
+    bins = np.linspace(0, end.max(), 41)
     inflight = [(int(((start <= t) & (end > t)).sum())) for t in bins]
     waves_live = [len(np.unique(wave[(start <= t) & (end > t)])) for t in bins]
     print("  t(us) rays-in-flight waves-live:")
