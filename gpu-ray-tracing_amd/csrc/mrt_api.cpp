@@ -43,6 +43,7 @@ struct mrt_tracer {
     // the LDS copy every workgroup makes (mrt::build_treetop). Rebuilt when the
     // BVH or the requested size changes.
     float4* top = nullptr;
+    int* topIdx = nullptr;
     int* topCountDev = nullptr;
     int topNodes = 0;       // nodes in the built treetop (0 = none)
     int topBuiltFor = -1;   // cfg.treetop_nodes it was built for
@@ -227,10 +228,11 @@ int refresh_treetop(mrt_tracer* t) {
     if (want > 0) {
         if (!t->top) {
             MRT_HIP(hipMalloc(&t->top, (size_t)mrt::kTopMaxNodes * 64));
+            MRT_HIP(hipMalloc(&t->topIdx, (size_t)mrt::kTopMaxNodes * sizeof(int)));
             MRT_HIP(hipMalloc(&t->topCountDev, sizeof(int)));
         }
-        MRT_HIP(mrt::build_treetop(static_cast<const float4*>(t->nodes), t->nodeBytes, t->top, want, t->topCountDev,
-                                   nullptr));
+        MRT_HIP(mrt::build_treetop(static_cast<const float4*>(t->nodes), t->nodeBytes, t->top, t->topIdx, want,
+                                   t->topCountDev, nullptr));
         int n = 0;
         MRT_HIP(hipMemcpy(&n, t->topCountDev, sizeof(int), hipMemcpyDeviceToHost));
         t->topNodes = n;
@@ -284,6 +286,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     a.status = ws->status;
     a.stats = reinterpret_cast<int4*>(stats);
     a.top = t->top;
+    a.topIdx = t->topIdx;
     a.topNodes = v.treetop ? t->topNodes : 0;
     a.rootAddr = v.treetop ? mrt::kTopTag : 0;
 
@@ -408,6 +411,7 @@ int mrt_tracer_destroy(mrt_tracer* t) {
     {
         DeviceGuard guard(t->device);
         if (t->top) (void)hipFree(t->top);
+        if (t->topIdx) (void)hipFree(t->topIdx);
         if (t->topCountDev) (void)hipFree(t->topCountDev);
         for (mrt::Workspace* w : t->workspaces) {
             if (w->stream) (void)hipStreamSynchronize(static_cast<hipStream_t>(w->stream));

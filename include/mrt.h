@@ -73,7 +73,7 @@ typedef struct mrt_launch_cfg {
                                   dynamic fetch: a static first round, then one atomic per wave refill
                                   on the queue of the wave's XCD (xcc % num_queues), no stealing      */
     int32_t lds_stack;         /* traversal-stack entries per lane kept in LDS: 8, 16 or 32       */
-    int32_t treetop_nodes;     /* nodes of the BVH's top levels (breadth-first from the root, <= 352) that
+    int32_t treetop_nodes;     /* nodes of the BVH's top levels (breadth-first from the root, <= 320) that
                                   every workgroup copies to LDS and reads there instead of L1/L2;
                                   0 = off, -1 = library default. Results are unchanged (same node bytes) */
     int32_t lane_groups;       /* strided mode: a wave's 64 lanes take rays from this many (1..64, power of

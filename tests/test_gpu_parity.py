@@ -173,10 +173,10 @@ def test_exact_reciprocal_is_correctly_rounded_for_every_float(tracer):
                                  dict(num_queues=1), dict(num_queues=8, fetch_threshold=40),
                                  dict(num_queues=8, waves_per_cu=32, fetch_threshold=64),
                                  dict(num_queues=-1, fetch_threshold=16), dict(num_queues=-1, waves_per_cu=4),
-                                 dict(waves_per_cu=4, lds_stack=8, num_queues=3), dict(treetop_nodes=352),
+                                 dict(waves_per_cu=4, lds_stack=8, num_queues=3), dict(treetop_nodes=320),
                                  dict(treetop_nodes=1), dict(treetop_nodes=3, lds_stack=8, num_queues=3),
                                  dict(treetop_nodes=200, lds_stack=32, waves_per_cu=4, fetch_threshold=48),
-                                 dict(treetop_nodes=352, lane_groups=8), dict(lane_groups=2),
+                                 dict(treetop_nodes=320, lane_groups=8), dict(lane_groups=2),
                                  dict(lane_groups=8), dict(lane_groups=64, waves_per_cu=4)],
                          ids=lambda c: ",".join(f"{k}={v}" for k, v in c.items()))
 def test_launch_configs_do_not_change_results(tracer, cfg):
@@ -192,7 +192,7 @@ def test_launch_configs_do_not_change_results(tracer, cfg):
         tracer.set_config(**saved)
 
 
-@pytest.mark.parametrize("top", [352, 17])
+@pytest.mark.parametrize("top", [320, 17])
 @pytest.mark.parametrize("wl", WORKLOADS, ids=lambda w: "-".join(map(str, w)))
 def test_treetop_is_bit_identical(tracer, wl, top):
     """treetop_nodes: the BVH's top levels read from an LDS copy (tagged child
@@ -219,7 +219,7 @@ def test_treetop_with_deep_stacks_and_rebinding(tracer):
     (the treetop is rebuilt per bind) + known answers on hand-built trees."""
     saved = tracer.config()
     try:
-        tracer.set_config(treetop_nodes=352, lds_stack=8)
+        tracer.set_config(treetop_nodes=320, lds_stack=8)
         test_rebinding_a_different_bvh(tracer)
         bufs, rays, any_hit, want, st = scene_setup("sponza", 256, 192, "diffuse")
         res, gst = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=False, stats=True)
@@ -309,7 +309,7 @@ def test_invalid_config_rejected(tracer):
     with pytest.raises(MrtError):
         tracer.set_config(num_queues=9)
     with pytest.raises(MrtError):
-        tracer.set_config(treetop_nodes=353)
+        tracer.set_config(treetop_nodes=321)
     with pytest.raises(MrtError):
         tracer.set_config(lane_groups=3)
 
