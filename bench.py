@@ -582,7 +582,6 @@ def main():
     ap.add_argument("--fetch-threshold", type=int, default=-1)
     ap.add_argument("--lds-stack", type=int, default=0)
     ap.add_argument("--queues", type=int, default=0)
-    ap.add_argument("--treetop", type=int, default=-1, help="treetop nodes in LDS (0 off, -1 library default)")
     ap.add_argument("--bvh-cache", default=os.path.join(os.environ.get("TMPDIR", "/tmp"), "mrt_bvhcache"),
                     help="directory of Compact2 .dat caches (built if missing); '' disables")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -603,8 +602,6 @@ def main():
         cfg["lds_stack"] = args.lds_stack
     if args.queues:
         cfg["num_queues"] = args.queues
-    if args.treetop >= 0:
-        cfg["treetop_nodes"] = args.treetop
     if args.lane_groups:
         cfg["lane_groups"] = args.lane_groups
     if cfg:

@@ -39,15 +39,6 @@ struct mrt_tracer {
 
     mrt_launch_cfg cfg{};
 
-    // Treetop (cfg.treetop_nodes > 0): the bound BVH's top levels, tagged for
-    // the LDS copy every workgroup makes (mrt::build_treetop). Rebuilt when the
-    // BVH or the requested size changes.
-    float4* top = nullptr;
-    int* topIdx = nullptr;
-    int* topCountDev = nullptr;
-    int topNodes = 0;       // nodes in the built treetop (0 = none)
-    int topBuiltFor = -1;   // cfg.treetop_nodes it was built for
-
     // Launch scratch, one set per stream the handle has launched on: the stack
     // spill slab, the queue heads and the overflow counter are written by a
     // running trace, so two traces in flight on different streams must not
@@ -57,7 +48,7 @@ struct mrt_tracer {
 
     // Occupancy per kernel variant, queried once (hipOccupancy* is a host
     // round-trip that would otherwise sit on every launch).
-    int occ[256] = {};
+    int occ[64] = {};
 
 };
 
@@ -115,7 +106,6 @@ mrt_launch_cfg default_cfg() {
     c.fetch_threshold = 0;   // strided mode: a wave refills once all its lanes are done
     c.num_queues = -1;       // static strided assignment (see trace_kernel.hip); 1..8 = atomic queues
     c.lds_stack = 16;
-    c.treetop_nodes = 0;
     c.lane_groups = 1;
     return c;
 }
@@ -124,7 +114,6 @@ bool valid_cfg(const mrt_launch_cfg& c) {
     return (c.waves_per_cu == 0 || (c.waves_per_cu >= 4 && c.waves_per_cu <= 32)) && c.fetch_threshold >= 0 && c.fetch_threshold <= 64 &&
            (c.num_queues == -1 || (c.num_queues >= 1 && c.num_queues <= mrt::kMaxQueues)) &&
            (c.lds_stack == 8 || c.lds_stack == 16 || c.lds_stack == 32) &&
-           c.treetop_nodes >= 0 && c.treetop_nodes <= mrt::kTopMaxNodes &&
            c.lane_groups >= 1 && c.lane_groups <= 64 && (c.lane_groups & (c.lane_groups - 1)) == 0;
 }
 
@@ -135,7 +124,6 @@ mrt::TraceVariant variant_for(const mrt_tracer* t, uint32_t flags) {
     v.speculative = (flags & MRT_TRACE_LOCKSTEP_OFF) == 0;
     v.stats = (flags & MRT_TRACE_STATS) != 0;
     v.ldsStack = t->cfg.lds_stack;
-    v.treetop = t->topNodes > 0;
     return v;
 }
 
@@ -155,8 +143,7 @@ constexpr int kAutoMinWaves = 8;
 // workgroup is resident at once.
 int variant_key(const mrt::TraceVariant& v) {
     const int lds = v.ldsStack == 8 ? 0 : v.ldsStack == 16 ? 1 : 2;
-    return (v.anyHit ? 1 : 0) | (v.speculative ? 2 : 0) | (v.exactRcp ? 4 : 0) | (v.stats ? 8 : 0) | (lds << 4) |
-           (v.treetop ? 64 : 0);
+    return (v.anyHit ? 1 : 0) | (v.speculative ? 2 : 0) | (v.exactRcp ? 4 : 0) | (v.stats ? 8 : 0) | (lds << 4);
 }
 
 int grid_blocks(mrt_tracer* t, const mrt::TraceVariant& v, int numRays, int* outBlocksPerCU) {
@@ -215,32 +202,6 @@ int workspace_for(mrt_tracer* t, void* stream, int totalLanes, int ldsStack, mrt
     return MRT_OK;
 }
 
-// (Re)builds the treetop for the bound BVH and the configured size; called by
-// bind and set_config with the handle's mutex held. Synchronous: launches in
-// flight may still read the previous treetop, so the device is drained first.
-int refresh_treetop(mrt_tracer* t) {
-    const int want = t->bound ? t->cfg.treetop_nodes : 0;
-    if (want == t->topBuiltFor) return MRT_OK;
-    DeviceGuard guard(t->device);
-    MRT_HIP(hipDeviceSynchronize());
-    t->topNodes = 0;
-    t->topBuiltFor = -1;
-    if (want > 0) {
-        if (!t->top) {
-            MRT_HIP(hipMalloc(&t->top, (size_t)mrt::kTopMaxNodes * 64));
-            MRT_HIP(hipMalloc(&t->topIdx, (size_t)mrt::kTopMaxNodes * sizeof(int)));
-            MRT_HIP(hipMalloc(&t->topCountDev, sizeof(int)));
-        }
-        MRT_HIP(mrt::build_treetop(static_cast<const float4*>(t->nodes), t->nodeBytes, t->top, t->topIdx, want,
-                                   t->topCountDev, nullptr));
-        int n = 0;
-        MRT_HIP(hipMemcpy(&n, t->topCountDev, sizeof(int), hipMemcpyDeviceToHost));
-        t->topNodes = n;
-    }
-    t->topBuiltFor = want;
-    return MRT_OK;
-}
-
 // Largest batch one launch takes: ray/result addressing and the strided round
 // arithmetic stay inside int32 with room for the grid (bigger batches are split
 // by the caller, as the reference Renderer does at 2^21 rays, Renderer.cc:46).
@@ -285,10 +246,6 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     a.spill = ws->spill;
     a.status = ws->status;
     a.stats = reinterpret_cast<int4*>(stats);
-    a.top = t->top;
-    a.topIdx = t->topIdx;
-    a.topNodes = v.treetop ? t->topNodes : 0;
-    a.rootAddr = v.treetop ? mrt::kTopTag : 0;
 
     hipStream_t s = static_cast<hipStream_t>(stream);
     // Queue heads restart at zero for every launch; strided mode has none.
@@ -306,7 +263,6 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
         info->grid_waves = totalLanes / 64;
         info->block_threads = mrt::kBlockThreads;
         info->lds_stack_entries = v.ldsStack;
-        info->treetop_nodes = v.treetop ? t->topNodes : 0;
         int overflow = 0;
         MRT_HIP(hipMemcpy(&overflow, ws->status, sizeof(int), hipMemcpyDeviceToHost));
         info->stack_overflows = overflow;
@@ -410,9 +366,6 @@ int mrt_tracer_destroy(mrt_tracer* t) {
     if (!t) return MRT_OK;
     {
         DeviceGuard guard(t->device);
-        if (t->top) (void)hipFree(t->top);
-        if (t->topIdx) (void)hipFree(t->topIdx);
-        if (t->topCountDev) (void)hipFree(t->topCountDev);
         for (mrt::Workspace* w : t->workspaces) {
             if (w->stream) (void)hipStreamSynchronize(static_cast<hipStream_t>(w->stream));
             if (w->queues) (void)hipFree(w->queues);
@@ -444,8 +397,7 @@ int mrt_tracer_bind(mrt_tracer* t, const void* nodes, int64_t nodeBytes, const v
     t->triIndex = triIndex;
     t->triIndexBytes = triIndexBytes;
     t->bound = true;
-    t->topBuiltFor = -1;   // a new BVH: its treetop is built now (if configured)
-    return refresh_treetop(t);
+    return MRT_OK;
 }
 
 int mrt_tracer_unbind(mrt_tracer* t) {
@@ -454,7 +406,7 @@ int mrt_tracer_unbind(mrt_tracer* t) {
     t->bound = false;
     t->nodes = t->woop = nullptr;
     t->triIndex = nullptr;
-    return refresh_treetop(t);
+    return MRT_OK;
 }
 
 int mrt_tracer_set_config(mrt_tracer* t, const mrt_launch_cfg* cfg) {
@@ -464,12 +416,11 @@ int mrt_tracer_set_config(mrt_tracer* t, const mrt_launch_cfg* cfg) {
     if (c.waves_per_cu == 0) c.waves_per_cu = d.waves_per_cu;
     if (c.num_queues == 0) c.num_queues = d.num_queues;
     if (c.lds_stack == 0) c.lds_stack = d.lds_stack;
-    if (c.treetop_nodes < 0) c.treetop_nodes = d.treetop_nodes;   // -1 = library default, 0 = off
     if (c.lane_groups == 0) c.lane_groups = d.lane_groups;
     if (!valid_cfg(c)) return fail(MRT_ERR_INVALID_ARG, "launch config out of range");
     std::lock_guard<std::mutex> lock(t->mu);
     t->cfg = c;
-    return refresh_treetop(t);
+    return MRT_OK;
 }
 
 int mrt_tracer_get_config(const mrt_tracer* t, mrt_launch_cfg* cfg) {

@@ -18,12 +18,7 @@ constexpr int kStackCapacity = 64;
 constexpr int kMaxQueues = 8;
 constexpr int kQueueStrideWords = 64;      // one 256-B line per queue head
 constexpr int kBlockThreads = 256;         // 4 wave64s per workgroup
-// Treetop: child pointers into the LDS copy of the BVH's top levels are
-// kTopTag + 4 * slot (above every Compact2 float4 index, below the sentinel).
-constexpr int kTopTag = 0x40000000;
-constexpr int kTopMaxNodes = 320;          // 20 KB node copy + 1.25 KB index table per workgroup (+ an 8-entry stack: 5 workgroups/CU)
-// Largest node / woop buffer a tracer binds: offsets above it are out of range
-// for every buffer (the kernel's "no step" loads use 0xFFFFFFC0).
+// Largest node / woop buffer a tracer binds (32-bit buffer offsets).
 constexpr int64_t kMaxBufferBytes = 0xFFFFFFC0ll;
 
 // Everything one launch needs; passed by value as the kernel argument.
@@ -44,10 +39,6 @@ struct TraceArgs {
     int* spill;                // (kStackCapacity - S) * totalLanes ints
     int* status;               // [0] = stack overflow count (lanes that pushed past kStackCapacity)
     int4* stats;               // per-ray {nodes, tris, leaves, 0} (STATS variants)
-    const float4* top;         // treetop nodes (topNodes x 64 B), child pointers tagged
-    const int* topIdx;         // treetop slot -> the node's Compact2 float4 index
-    int topNodes;              // 0 = no treetop
-    int rootAddr;              // first node: 0, or kTopTag (the treetop's root)
 };
 
 // Variant selector (all combinations are instantiated in trace_kernel.hip).
@@ -57,16 +48,10 @@ struct TraceVariant {
     bool exactRcp;      // IEEE 1/x vs v_rcp_f32
     bool stats;
     int ldsStack;       // 8, 16 or 32 LDS entries per lane
-    bool treetop;       // the top BVH levels are read from an LDS copy
 };
 
 // Launch one persistent trace. grid = number of 256-thread workgroups.
 hipError_t launch_trace(const TraceVariant& v, const TraceArgs& a, int gridBlocks, hipStream_t s);
-
-// Builds the treetop of a bound BVH into `top` (maxNodes <= kTopMaxNodes nodes);
-// *countDev = nodes written. One workgroup, stream-ordered.
-hipError_t build_treetop(const float4* nodes, int64_t nodeBytes, float4* top, int* topIdx, int maxNodes,
-                         int* countDev, hipStream_t s);
 
 // Resident 256-thread workgroups per CU for a variant (occupancy query).
 hipError_t trace_occupancy(const TraceVariant& v, int* blocksPerCU);

@@ -73,9 +73,6 @@ typedef struct mrt_launch_cfg {
                                   dynamic fetch: a static first round, then one atomic per wave refill
                                   on the queue of the wave's XCD (xcc % num_queues), no stealing      */
     int32_t lds_stack;         /* traversal-stack entries per lane kept in LDS: 8, 16 or 32       */
-    int32_t treetop_nodes;     /* nodes of the BVH's top levels (breadth-first from the root, <= 320) that
-                                  every workgroup copies to LDS and reads there instead of L1/L2;
-                                  0 = off, -1 = library default. Results are unchanged (same node bytes) */
     int32_t lane_groups;       /* strided mode: a wave's 64 lanes take rays from this many (1..64, power of
                                   two) distant sub-ranges of the batch instead of 64 consecutive rays */
 } mrt_launch_cfg;
@@ -88,7 +85,6 @@ typedef struct mrt_trace_info {
     int32_t lds_stack_entries; /* per-lane traversal-stack entries held in LDS                    */
     int32_t stack_overflows;   /* pushes past the 64-entry stack in this launch (then the call returns
                                   MRT_ERR_STACK_OVERFLOW; 0 for any SBVH of depth <= 64)            */
-    int32_t treetop_nodes;     /* treetop nodes the launch read from LDS (0 = treetop off)        */
 } mrt_trace_info;
 
 /* ---- handle API -------------------------------------------------------- */
