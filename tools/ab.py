@@ -43,7 +43,7 @@ def load(libdir):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="bunny-primary-1024x768")
+    ap.add_argument("--workload", action="append", help="repeatable")
     ap.add_argument("--variant", action="append", required=True, help="libdir:json-config")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=20)
@@ -51,14 +51,22 @@ def main():
     args = ap.parse_args()
 
     import torch
+    torch.cuda.set_device(0)
+    for wl in args.workload or ["bunny-primary-1024x768"]:
+        run(args, wl)
+
+
+def run(args, workload):
+    import torch
     import bench
     from mrt import _lib
     from mrt.tracer import Tracer
-    torch.cuda.set_device(0)
+    args.workload = workload
     scene_name = bench.workload_spec(args.workload)[0]
-    scene, bufs, _, _ = bench.bvh_for(scene_name, 1, 0)
-    b = bench.Batches(args.workload, scene, bufs, Tracer(0))
-    g = b.gbvh
+    scenes = bench.SceneCache(1, 0, os.path.join(os.environ.get("TMPDIR", "/tmp"), "mrt_bvhcache"))
+    e = scenes.get(scene_name)
+    b = bench.Batches(args.workload, e["scene"], e["gbvh"], Tracer(0))
+    g = e["gbvh"]
     stream = torch.cuda.current_stream()
     variants = []
     for spec in args.variant:
