@@ -1,11 +1,14 @@
 // host_api.cpp — the C-ABI of include/mrt_host.h over the host C++ pieces.
+#include <cstdio>
 #include <cstring>
+#include <vector>
 #include <exception>
 #include <memory>
 #include <string>
 
 #include "../../../include/mrt_host.h"
 #include "bvh.hpp"
+#include "fwhash.hpp"
 #include "raygen.hpp"
 #include "scene.hpp"
 
@@ -112,6 +115,43 @@ int mrth_scene_tri_colors(const mrth_scene* s, uint32_t* material, uint32_t* sha
             shaded[i] = host_to_abgr(c);
         }
     }
+    return MRTH_OK;
+}
+
+uint32_t mrth_fw_hash_buffer(const void* ptr, int64_t size) {
+    return (ptr || size == 0) && size >= 0 ? mrt::fw::hash_buffer(ptr, size) : 0u;
+}
+
+uint32_t mrth_scene_hash(const mrth_scene* s) {
+    if (!s) return 0;
+    // Scene::hash (Scene.cc:93-101) over the five buffers Scene::Scene fills (:37-80).
+    const mrt::Scene& sc = s->scene;
+    const size_t nt = sc.triangles.size();
+    std::vector<uint32_t> material(nt), shaded(nt);
+    mrth_scene_tri_colors(s, material.data(), shaded.data());
+    using mrt::fw::hash_buffer;
+    static_assert(sizeof(mrt::Vec3i) == 12 && sizeof(mrt::Vec3f) == 12, "Scene buffers are packed 12-byte records");
+    return mrt::fw::hash_bits6(hash_buffer(sc.triangles.data(), (int64_t)nt * 12),
+                               hash_buffer(sc.triNormals.data(), (int64_t)sc.triNormals.size() * 12),
+                               hash_buffer(material.data(), (int64_t)nt * 4), hash_buffer(shaded.data(), (int64_t)nt * 4),
+                               hash_buffer(sc.vertices.data(), (int64_t)sc.vertices.size() * 12));
+}
+
+int mrth_bvh_cache_name(const mrth_scene* s, const mrth_build_params* p, char out[16]) {
+    if (!s || !out) return fail(MRTH_ERR_INVALID_ARG, "null argument");
+    mrth_build_params d;
+    mrth_default_build_params(&d);
+    if (!p) p = &d;
+    using namespace mrt::fw;
+    // Platform("GPU") with setLeafPreferences(min, max) (Renderer.cc:53-54; Platform.hh:43,69):
+    // hashBits(hash<String>(name), costs, hashBits(triBatch 1, nodeBatch 1, minLeaf, maxLeaf)).
+    const uint32_t platform = hash_bits6(hash_buffer("GPU", 3), float_bits(p->sah_node_cost),
+                                         float_bits(p->sah_triangle_cost),
+                                         hash_bits6(1u, 1u, (uint32_t)p->min_leaf_size, (uint32_t)p->max_leaf_size));
+    const uint32_t params = hash_bits(float_bits(p->split_alpha));   // BVH::BuildParams::computeHash (BVH.hh:82-85)
+    const uint32_t kLayoutCompact2 = 5;                              // BVHLayout_Compact2 (CudaTracerKernels.hh:124)
+    const uint32_t h = hash_bits6(mrth_scene_hash(s), platform, params, kLayoutCompact2);
+    std::snprintf(out, 16, "%08x.dat", h);   // Renderer.cc:180
     return MRTH_OK;
 }
 
@@ -260,6 +300,23 @@ int mrth_primary_rays_subpixel(const mrth_camera* cam, int32_t w, int32_t h, flo
     if (!cam || w <= 0 || h <= 0 || !rays) return fail(MRTH_ERR_INVALID_ARG, "bad arguments");
     if (!(jx >= 0.0f && jx < 1.0f && jy >= 0.0f && jy < 1.0f)) return fail(MRTH_ERR_INVALID_ARG, "subpixel offset outside [0, 1)");
     mrt::gen_primary_rays(to_camera(cam), w, h, static_cast<mrt::Ray*>(rays), slotToId, jx, jy);
+    return MRTH_OK;
+}
+
+int mrth_camera_decode_signature(const char* sig, mrth_camera* cam, float* speed, int32_t* keepAligned) {
+    if (!sig || !cam) return fail(MRTH_ERR_INVALID_ARG, "bad arguments");
+    mrt::CameraSignature c;
+    if (!mrt::decode_camera_signature(sig, &c)) return fail(MRTH_ERR_INVALID_ARG, "CameraControls: Invalid signature!");
+    for (int i = 0; i < 3; i++) {
+        cam->position[i] = c.position[i];
+        cam->forward[i] = c.forward[i];
+        cam->up[i] = c.up[i];
+    }
+    cam->fov_deg = c.fov;
+    cam->near_dist = c.nearDist;
+    cam->far_dist = c.farDist;
+    if (speed) *speed = c.speed;
+    if (keepAligned) *keepAligned = c.keepAligned ? 1 : 0;
     return MRTH_OK;
 }
 

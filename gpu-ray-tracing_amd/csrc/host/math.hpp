@@ -153,4 +153,13 @@ inline Mat4f inverted(const Mat4f& a) {
     return r;
 }
 
+// A decoded camera signature (CameraControls m_position .. m_keepAligned,
+// CameraControls.cc:374-419); camera.cpp.
+struct CameraSignature {
+    Vec3f position, forward, up;
+    float speed = 0.f, fov = 0.f, nearDist = 0.f, farDist = 0.f;
+    bool keepAligned = false;
+};
+bool decode_camera_signature(const char* sig, CameraSignature* out);
+
 }  // namespace mrt

@@ -1,20 +1,38 @@
-// obj_io.cpp — Wavefront OBJ import into a flattened Scene.
+// obj_io.cpp — Wavefront OBJ (+ MTL) import into a flattened Scene.
 //
-// Follows the reference's importer (src/framework/io/MeshWavefrontIO.cc:258-467)
-// where it affects the triangle ids the tracer reports: polygons are
-// fan-triangulated as (v0, v[i-1], v[i]) (:359-360), indices may be negative
-// (relative to the current end of the list), and triangles are grouped per
-// material submesh in order of first use, then flattened submesh by submesh
-// (reference src/rt/Scene.cc:63-82). Texture coordinates and normals are parsed
-// and ignored: the tracer only needs positions.
+// Restates the reference importer (src/framework/io/MeshWavefrontIO.cc:97-467)
+// wherever it decides the Scene's bytes, because those bytes decide the BVH, the
+// triangle ids the tracer reports and the bvhcache file name (Scene::hash,
+// Scene.cc:93-101):
+//   * lines as BufferedInputStream::readLine(true, true) returns them (Stream.cc:89-144):
+//     '\r' dropped, tabs turned into spaces, a trailing backslash joins the next line;
+//   * numbers through the framework's own parsers (String.cc:396-509): parseFloat
+//     accumulates digits in float32 (v*10 + d, then scale *= 0.1f; v += scale*d, then
+//     v *= powf(10, e)), which is not strtof — vertex bits follow the reference's;
+//   * "v x y z" with exactly three values, "vt" with at least two, "vn" with exactly three
+//     (other forms are invalid lines, skipped, and take no index);
+//   * face corners "p[/t[/n]]": indices relative to the lists read so far (negative from
+//     the end, 0 or out of range = none), one mesh vertex per distinct (p, t, n) triple in
+//     order of first use (the reference's vertexHash, :317-348) at position p (or the origin);
+//     polygons fan-triangulated (v0, v[i-1], v[i]) (:359-360); a corner that does not parse
+//     invalidates the face, but the corners before it still made their vertices;
+//   * submeshes: faces collect until a "usemtl" switches away; a usemtl naming a loaded
+//     material selects that material's submesh (created on first use), any other name
+//     selects none, so following faces join the default submesh (:350-384);
+//   * "mtllib" resolved against the OBJ's directory (String::getDirName: "." when none);
+//     "newmtl" of an existing name keeps the current material (:131-138); Kd writes the
+//     values it parsed even when the line is invalid (parseFloats writes as it goes).
+// Texture maps abort the reference (fail("parseTexture shouldn't be called")); here they
+// are ignored. Texture coordinates and normals only number vertices: the tracer needs
+// positions.
+#include <cmath>
 #include <cstdio>
-#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <array>
 #include <map>
-#include <sstream>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "scene.hpp"
@@ -23,160 +41,275 @@ namespace mrt {
 
 namespace {
 
-// One face index (reference :317-340): negative = relative to the current end
-// of the list; an index outside the list maps to -1 ("no vertex", which the
-// reference turns into a vertex at the origin) instead of failing the file.
-bool parse_index(const char*& p, int count, int* out) {
-    char* end = nullptr;
-    const long v = std::strtol(p, &end, 10);
-    if (end == p) return false;
-    p = end;
-    long idx = (v < 0) ? count + v : v - 1;
-    *out = (idx < 0 || idx >= count) ? -1 : (int)idx;
+// ---- BufferedInputStream::readLine(combineWithBackslash, normalizeWhitespace) ----
+class LineReader {
+public:
+    explicit LineReader(std::istream& in) : in_(in) {}
+    bool next(std::string& out) {
+        out.clear();
+        int c = in_.get();
+        if (c == EOF) return false;
+        bool pendingBackslash = false;
+        for (;; c = in_.get()) {
+            if (c == EOF) {
+                if (pendingBackslash) out.push_back('\\');
+                break;
+            }
+            const unsigned char chr = (unsigned char)c;
+            if (chr >= 32 && chr != '\\' && !pendingBackslash) {
+                out.push_back((char)chr);
+            } else if (chr == '\n') {
+                if (!pendingBackslash) break;
+                out.push_back(' ');
+                pendingBackslash = false;
+            } else if (chr != '\r') {
+                if (pendingBackslash) {
+                    out.push_back('\\');
+                    pendingBackslash = false;
+                }
+                if (chr == '\t') out.push_back(' ');
+                else if (chr == '\\') pendingBackslash = true;
+                else out.push_back((char)chr);
+            }
+        }
+        return true;
+    }
+
+private:
+    std::istream& in_;
+};
+
+// ---- the framework's parsers (String.cc:356-509, MeshWavefrontIO.cc:97-110) ----
+void parse_space(const char*& p) {
+    while (*p == ' ' || *p == '\t') p++;
+}
+
+bool parse_char(const char*& p, char c) {
+    if (*p != c) return false;
+    p++;
     return true;
 }
 
-// loadMtl (reference MeshWavefrontIO.cc:114-200): "newmtl" opens a material
-// (diffuse defaults to (0.75, 0.75, 0.75, 1), Mesh.hh:92), "Kd r g b" sets its
-// diffuse rgb, "d a" its alpha; the rest (Ka, Ks, Ns, maps) does not reach the
-// colour tables and is skipped.
-void load_mtl(const std::string& path, std::map<std::string, std::array<float, 4>>& mats) {
-    std::ifstream in(path);
-    if (!in) return;   // the reference ignores a missing library too
-    std::array<float, 4>* cur = nullptr;
+bool parse_literal(const char*& p, const char* s) {
+    const char* t = p;
+    while (*s && *t == *s) {
+        t++;
+        s++;
+    }
+    if (*s) return false;
+    p = t;
+    return true;
+}
+
+bool parse_int(const char*& p, int32_t& value) {
+    const char* t = p;
+    int32_t v = 0;
+    const bool neg = !parse_char(t, '+') && parse_char(t, '-');
+    if (*t < '0' || *t > '9') return false;
+    while (*t >= '0' && *t <= '9') v = (int32_t)((uint32_t)v * 10u + (uint32_t)(*t++ - '0'));
+    value = neg ? -v : v;
+    p = t;
+    return true;
+}
+
+bool parse_float(const char*& p, float& value) {
+    const char* t = p;
+    const bool neg = !parse_char(t, '+') && parse_char(t, '-');
+    float v = 0.0f;
+    int digits = 0;
+    while (*t >= '0' && *t <= '9') {
+        v = v * 10.0f + (float)(*t++ - '0');
+        digits++;
+    }
+    if (parse_char(t, '.')) {
+        float scale = 1.0f;
+        while (*t >= '0' && *t <= '9') {
+            scale *= 0.1f;
+            v += scale * (float)(*t++ - '0');
+            digits++;
+        }
+    }
+    if (!digits) return false;
+    p = t;
+    if (*p == '#') {
+        uint32_t bits = 0;
+        if (parse_literal(p, "#INF")) bits = neg ? 0xFF800000u : 0x7F800000u;
+        else if (parse_literal(p, "#SNAN")) bits = neg ? 0xFF800001u : 0x7F800001u;
+        else if (parse_literal(p, "#QNAN")) bits = neg ? 0xFFC00001u : 0x7FC00001u;
+        else if (parse_literal(p, "#IND")) bits = neg ? 0xFFC00000u : 0x7FC00000u;
+        if (bits) {
+            std::memcpy(&value, &bits, 4);
+            return true;
+        }
+    }
+    int32_t e = 0;
+    if ((parse_char(t, 'e') || parse_char(t, 'E')) && parse_int(t, e)) {
+        p = t;
+        if (e) v *= powf(10.0f, (float)e);
+    }
+    value = neg ? -v : v;
+    return true;
+}
+
+bool parse_floats(const char*& p, float* values, int num) {   // writes as it goes, like the reference
+    const char* t = p;
+    for (int i = 0; i < num; i++) {
+        if (i) parse_space(t);
+        if (!parse_float(t, values[i])) return false;
+    }
+    p = t;
+    return true;
+}
+
+// ---- loadMtl (MeshWavefrontIO.cc:114-250): the fields that reach Scene's colour tables ----
+using Material = std::array<float, 4>;   // diffuse rgba; default (0.75, 0.75, 0.75, 1) (Mesh.hh)
+
+void load_mtl(const std::string& path, std::map<std::string, Material>& mats) {
+    std::ifstream in(path, std::ios::binary);
+    if (!in) return;   // FileRO error: nothing loaded (the reference clears the error too)
+    LineReader lines(in);
     std::string line;
-    while (std::getline(in, line)) {
+    Material* mat = nullptr;
+    while (lines.next(line)) {
         const char* p = line.c_str();
-        while (*p == ' ' || *p == '\t') ++p;
-        if (std::strncmp(p, "newmtl ", 7) == 0) {
-            std::string name = p + 7;
-            name.erase(0, name.find_first_not_of(" \t"));
-            while (!name.empty() && (name.back() == '\r' || name.back() == ' ')) name.pop_back();
-            cur = &mats.emplace(name, std::array<float, 4>{0.75f, 0.75f, 0.75f, 1.0f}).first->second;
-        } else if (cur && std::strncmp(p, "Kd ", 3) == 0) {
-            float r, g, b;
-            if (std::sscanf(p + 3, "%f %f %f", &r, &g, &b) == 3) { (*cur)[0] = r; (*cur)[1] = g; (*cur)[2] = b; }
-        } else if (cur && std::strncmp(p, "d ", 2) == 0) {
-            float a;
-            if (std::sscanf(p + 2, "%f", &a) == 1) (*cur)[3] = a;
+        parse_space(p);
+        if (!*p || parse_literal(p, "#")) continue;
+        if (parse_literal(p, "newmtl ")) {
+            parse_space(p);
+            if (*p && !mats.count(p)) mat = &mats.emplace(p, Material{0.75f, 0.75f, 0.75f, 1.0f}).first->second;
+        } else if (!mat) {
+            continue;
+        } else if (parse_literal(p, "Kd ")) {
+            parse_space(p);
+            if (!parse_literal(p, "spectral ") && !parse_literal(p, "xyz ")) parse_floats(p, mat->data(), 3);
+        } else if (parse_literal(p, "d ")) {
+            parse_space(p);
+            parse_float(p, (*mat)[3]);
         }
     }
 }
 
+struct PtnHash {
+    size_t operator()(const std::array<int32_t, 3>& k) const {
+        return ((size_t)(uint32_t)k[0] * 0x9E3779B97F4A7C15ull) ^ ((size_t)(uint32_t)k[1] << 21) ^
+               ((size_t)(uint32_t)k[2] * 0xC2B2AE3D27D4EB4Full);
+    }
+};
+
 }  // namespace
 
 bool load_obj(const std::string& path, Scene& out, std::string* err) {
-    std::ifstream in(path);
+    std::ifstream in(path, std::ios::binary);
     if (!in) {
         if (err) *err = "cannot open " + path;
         return false;
     }
     out = Scene();
     out.name = path;
+    const size_t slash = path.find_last_of("/\\");
+    const std::string dir = slash == std::string::npos ? std::string(".") : path.substr(0, slash);   // getDirName
+
+    std::vector<Vec3f> positions;
+    int32_t texCount = 0, normalCount = 0;
+    std::unordered_map<std::array<int32_t, 3>, int32_t, PtnHash> vertexHash;
     std::vector<std::vector<Vec3i>> submeshes;
     std::map<std::string, int> materialSubmesh;
-    std::map<std::string, std::array<float, 4>> materials;
-    const size_t slash = path.find_last_of("/\\");
-    const std::string dir = slash == std::string::npos ? std::string(".") : path.substr(0, slash);   // String::getDirName
-    // Submesh bookkeeping of the reference (:258-395): faces collect in `pending`
-    // and are appended to the current submesh when a usemtl switches away from
-    // it (or at the end of the file). A usemtl naming a material of the loaded
-    // libraries selects that material's submesh (created on first use); any other
-    // name selects none, so the faces that follow join the default submesh (the
-    // one created by the first face seen without a material).
-    std::map<std::string, int>& matSubmesh = materialSubmesh;
+    std::map<std::string, Material> materials;
     int current = -1, defaultSubmesh = -1;
-    std::vector<Vec3i> pending;
+    std::vector<Vec3i> pending;   // the reference's indexTmp
     auto flush = [&]() {
         if (current != -1) submeshes[current].insert(submeshes[current].end(), pending.begin(), pending.end());
         pending.clear();
     };
-    int texCount = 0, normalCount = 0;
+    std::vector<int32_t> corners;
+
+    LineReader lines(in);
     std::string line;
-    auto trailing_blank = [](const char* p) {
-        while (*p == ' ' || *p == '\t' || *p == '\r') ++p;
-        return *p == 0;
-    };
-    while (std::getline(in, line)) {
+    while (lines.next(line)) {
         const char* p = line.c_str();
-        while (*p == ' ' || *p == '\t') ++p;
-        if (p[0] == 'v' && (p[1] == ' ' || p[1] == '\t')) {
-            // "v x y z" exactly (reference :276-283: a fourth value makes the line invalid, skipped)
-            float x, y, z;
-            int n = 0;
-            if (std::sscanf(p + 2, "%f %f %f%n", &x, &y, &z, &n) == 3 && trailing_blank(p + 2 + n))
-                out.vertices.emplace_back(x, y, z);
-        } else if (p[0] == 'v' && p[1] == 't') {
-            ++texCount;
-        } else if (p[0] == 'v' && p[1] == 'n') {
-            ++normalCount;
-        } else if (p[0] == 'f' && (p[1] == ' ' || p[1] == '\t')) {
-            p += 2;
-            std::vector<int> poly;
-            bool ok = true;
+        parse_space(p);
+        if (!*p || parse_literal(p, "#")) continue;
+        if (parse_literal(p, "v ")) {
+            parse_space(p);
+            float v[3];
+            if (parse_floats(p, v, 3)) {
+                parse_space(p);
+                if (!*p) positions.emplace_back(v[0], v[1], v[2]);
+            }
+        } else if (parse_literal(p, "vt ")) {
+            parse_space(p);
+            float v[2], dummy;
+            if (parse_floats(p, v, 2)) {
+                parse_space(p);
+                while (parse_float(p, dummy)) parse_space(p);
+                if (!*p) texCount++;
+            }
+        } else if (parse_literal(p, "vn ")) {
+            parse_space(p);
+            float v[3];
+            if (parse_floats(p, v, 3)) {
+                parse_space(p);
+                if (!*p) normalCount++;
+            }
+        } else if (parse_literal(p, "f ")) {
+            parse_space(p);
+            corners.clear();
             while (*p) {
-                while (*p == ' ' || *p == '\t' || *p == '\r') ++p;
-                if (!*p) break;
-                int vi = 0, dummy = 0;
-                if (!parse_index(p, (int)out.vertices.size(), &vi)) { ok = false; break; }
-                if (*p == '/') {   // skip /vt and /vn
-                    ++p;
-                    if (*p != '/' && !parse_index(p, texCount, &dummy)) { ok = false; break; }
-                    if (*p == '/') { ++p; if (!parse_index(p, normalCount, &dummy)) { ok = false; break; } }
+                std::array<int32_t, 3> ptn{0, 0, 0};
+                if (!parse_int(p, ptn[0])) break;
+                for (int i = 1; i < 4 && parse_literal(p, "/"); i++) {
+                    int32_t tmp = 0;
+                    parse_int(p, tmp);
+                    if (i < 3) ptn[i] = tmp;
                 }
-                poly.push_back(vi);   // -1: resolved to the origin vertex after the last 'v' line
-            }
-            if (!ok) continue;   // unparsable face: skipped, like the reference's invalid lines
-            if (current == -1) {
-                if (defaultSubmesh == -1) {
-                    defaultSubmesh = (int)submeshes.size();
-                    submeshes.emplace_back();
+                parse_space(p);
+                const int32_t size[3] = {(int32_t)positions.size(), texCount, normalCount};
+                for (int i = 0; i < 3; i++) {
+                    if (ptn[i] < 0) ptn[i] += size[i];
+                    else ptn[i]--;
+                    if (ptn[i] < 0 || ptn[i] >= size[i]) ptn[i] = -1;
                 }
-                current = defaultSubmesh;
+                auto it = vertexHash.find(ptn);
+                if (it == vertexHash.end()) {
+                    it = vertexHash.emplace(ptn, (int32_t)out.vertices.size()).first;
+                    out.vertices.push_back(ptn[0] == -1 ? Vec3f(0.0f) : positions[ptn[0]]);
+                }
+                corners.push_back(it->second);
             }
-            for (size_t i = 2; i < poly.size(); i++) pending.push_back(Vec3i{poly[0], poly[i - 1], poly[i]});
-        } else if (std::strncmp(p, "mtllib ", 7) == 0) {
-            std::string name = p + 7;
-            name.erase(0, name.find_first_not_of(" \t"));
-            while (!name.empty() && (name.back() == '\r' || name.back() == ' ')) name.pop_back();
-            // Resolved against the OBJ's directory (:386-397); a missing library loads nothing.
-            if (!name.empty()) load_mtl(dir + "/" + name, materials);
-        } else if (std::strncmp(p, "usemtl ", 7) == 0) {
-            std::string name = p + 7;
-            name.erase(0, name.find_first_not_of(" \t"));
-            while (!name.empty() && (name.back() == '\r' || name.back() == ' ')) name.pop_back();
+            if (!*p) {
+                if (current == -1) {
+                    if (defaultSubmesh == -1) {
+                        defaultSubmesh = (int)submeshes.size();
+                        submeshes.emplace_back();
+                    }
+                    current = defaultSubmesh;
+                }
+                for (size_t i = 2; i < corners.size(); i++) pending.push_back(Vec3i{corners[0], corners[i - 1], corners[i]});
+            }
+        } else if (parse_literal(p, "usemtl ")) {
+            parse_space(p);
             flush();
             current = -1;
-            if (materials.count(name)) {
-                auto it = matSubmesh.find(name);
-                if (it == matSubmesh.end()) {
-                    it = matSubmesh.emplace(name, (int)submeshes.size()).first;
+            if (materials.count(p)) {
+                auto it = materialSubmesh.find(p);
+                if (it == materialSubmesh.end()) {
+                    it = materialSubmesh.emplace(p, (int)submeshes.size()).first;
                     submeshes.emplace_back();
                 }
                 current = it->second;
             }
+        } else if (parse_literal(p, "mtllib ")) {
+            parse_space(p);
+            if (*p) load_mtl(dir + "/" + p, materials);
         }
     }
     flush();
-    // Index -1 is the reference's vertex at the origin (:345-347); it is appended
-    // after every position, so it does not shift the relative indices above.
-    bool needOrigin = false;
-    for (auto& sm : submeshes)
-        for (auto& t : sm)
-            for (int k = 0; k < 3; k++) needOrigin |= t[k] < 0;
-    if (needOrigin) {
-        const int origin = (int)out.vertices.size();
-        out.vertices.emplace_back(0.f, 0.f, 0.f);
-        for (auto& sm : submeshes)
-            for (auto& t : sm)
-                for (int k = 0; k < 3; k++)
-                    if (t[k] < 0) t[k] = origin;
-    }
-    std::vector<std::array<float, 4>> smDiffuse(submeshes.size(), std::array<float, 4>{0.75f, 0.75f, 0.75f, 1.0f});
+
+    std::vector<Material> smDiffuse(submeshes.size(), Material{0.75f, 0.75f, 0.75f, 1.0f});
     bool anyMaterial = false;
     for (const auto& kv : materialSubmesh) {
-        auto m = materials.find(kv.first);
-        if (m != materials.end()) { smDiffuse[kv.second] = m->second; anyMaterial = true; }
+        smDiffuse[kv.second] = materials[kv.first];
+        anyMaterial = true;
     }
     for (size_t i = 0; i < submeshes.size(); i++) {
         out.triangles.insert(out.triangles.end(), submeshes[i].begin(), submeshes[i].end());

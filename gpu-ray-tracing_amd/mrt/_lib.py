@@ -102,6 +102,9 @@ HOST_SYMBOLS = [
     ("mrth_scene_camera", i32, [vp, C.POINTER(HostCamera), C.POINTER(f32)]),
     ("mrth_scene_tri_colors", i32, [vp, vp, vp]),
     ("mrth_default_build_params", None, [C.POINTER(BuildParams)]),
+    ("mrth_fw_hash_buffer", u32, [vp, i64]),
+    ("mrth_scene_hash", u32, [vp]),
+    ("mrth_bvh_cache_name", i32, [vp, C.POINTER(BuildParams), C.c_char_p]),
     ("mrth_bvh_build", i32, [vp, C.POINTER(BuildParams), C.POINTER(vp)]),
     ("mrth_bvh_load", i32, [C.c_char_p, C.POINTER(vp)]),
     ("mrth_bvh_save", i32, [vp, C.c_char_p]),
@@ -115,6 +118,7 @@ HOST_SYMBOLS = [
     ("mrth_primary_rays", i32, [C.POINTER(HostCamera), i32, i32, vp, vp]),
     ("mrth_primary_rays_subpixel", i32, [C.POINTER(HostCamera), i32, i32, f32, f32, vp, vp]),
     ("mrth_camera_nscreen_to_world", i32, [C.POINTER(HostCamera), i32, i32, C.POINTER(f32)]),
+    ("mrth_camera_decode_signature", i32, [C.c_char_p, C.POINTER(HostCamera), C.POINTER(f32), C.POINTER(i32)]),
     ("mrth_ao_rays", i32, [vp, vp, i64, vp, i32, f32, u32, vp]),
     ("mrth_count_hits", i64, [vp, i64]),
     ("mrth_last_error", C.c_char_p, []),

@@ -34,6 +34,19 @@ class Camera:
     near: float
     far: float
 
+    @classmethod
+    def from_signature(cls, sig: str) -> "Camera":
+        """CameraControls::decodeSignature (CameraControls.cc:374-419): the reference App's
+        --camera text, e.g. the signatures of grtcmdline.txt. The signature's speed and
+        keepAligned are kept as attributes."""
+        c = _lib.HostCamera()
+        speed, keep = C.c_float(), C.c_int32()
+        _lib.check_host(_lib.host_lib().mrth_camera_decode_signature(sig.encode(), C.byref(c), C.byref(speed),
+                                                                     C.byref(keep)))
+        cam = cls(tuple(c.position), tuple(c.forward), tuple(c.up), c.fov_deg, c.near_dist, c.far_dist)
+        cam.speed, cam.keep_aligned = float(speed.value), bool(keep.value)
+        return cam
+
     def to_c(self) -> _lib.HostCamera:
         c = _lib.HostCamera()
         for i in range(3):
@@ -96,6 +109,10 @@ class Scene:
         _lib.check_host(_lib.host_lib().mrth_scene_copy_arrays(self._h, _ptr(v), _ptr(t), _ptr(n)))
         return v, t, n
 
+    def hash(self) -> int:
+        """Scene::hash (Scene.cc:93-101)."""
+        return int(_lib.host_lib().mrth_scene_hash(self._h))
+
     def tri_colors(self):
         """(material, shaded) ABGR uint32 per triangle (Scene::Scene, reference Scene.cc:47-80)."""
         nt = self.num_triangles
@@ -127,6 +144,36 @@ class Bvh:
         h = C.c_void_p()
         _lib.check_host(_lib.host_lib().mrth_bvh_build(scene.handle, C.byref(p), C.byref(h)))
         return cls(h.value)
+
+    @staticmethod
+    def _params(max_leaf=8, min_leaf=1, split_alpha=1e-5, threads=0):
+        p = _lib.BuildParams()
+        _lib.host_lib().mrth_default_build_params(C.byref(p))
+        p.max_leaf_size, p.min_leaf_size, p.split_alpha, p.threads = max_leaf, min_leaf, split_alpha, threads
+        return p
+
+    @classmethod
+    def cache_name(cls, scene: Scene, max_leaf: int = 8, min_leaf: int = 1, split_alpha: float = 1e-5) -> str:
+        """The reference's bvhcache file name for this scene and build, "%08x.dat" of
+        hashBits(scene, platform, build params, layout) (Renderer.cc:178-186)."""
+        buf = C.create_string_buffer(16)
+        _lib.check_host(_lib.host_lib().mrth_bvh_cache_name(scene.handle, C.byref(cls._params(max_leaf, min_leaf,
+                                                                                              split_alpha)), buf))
+        return buf.value.decode()
+
+    @classmethod
+    def load_or_build(cls, scene: Scene, cache_dir: str = "bvhcache", **build) -> "Bvh":
+        """Renderer::getCudaBVH (Renderer.cc:157-217): read <cache_dir>/<cache_name>.dat when it
+        exists, otherwise build the SBVH and write it there (creating the directory)."""
+        import os
+        build_keys = {k: build[k] for k in ("max_leaf", "min_leaf", "split_alpha") if k in build}
+        path = os.path.join(cache_dir, cls.cache_name(scene, **build_keys))
+        if os.path.exists(path):
+            return cls.load(path)
+        bvh = cls.build(scene, **build)
+        os.makedirs(cache_dir, exist_ok=True)
+        bvh.save(path)
+        return bvh
 
     @classmethod
     def load(cls, path: str) -> "Bvh":

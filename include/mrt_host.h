@@ -73,6 +73,16 @@ int  mrth_scene_tri_colors(const mrth_scene* s, uint32_t* material, uint32_t* sh
 
 /* ---- BVH (SBVH build -> Compact2 host buffers) ---------------------------- */
 void mrth_default_build_params(mrth_build_params* p);
+
+/* hashBuffer (Hash.cc:34-76), the framework hash the two functions below are built on. */
+uint32_t mrth_fw_hash_buffer(const void* ptr, int64_t size);
+/* Scene::hash (Scene.cc:93-101): the framework hash (Hash.cc:34-76) of the scene's five
+ * buffers — triangle vertex indices, face normals, material and shaded colours, positions. */
+uint32_t mrth_scene_hash(const mrth_scene* s);
+/* The reference's bvhcache file name for this scene and build (Renderer.cc:178-186):
+ * "%08x.dat" of hashBits(scene hash, Platform("GPU") hash, BuildParams hash, BVHLayout_Compact2),
+ * written to out (>= 13 bytes; 16 are touched). p NULL = defaults (mrth_default_build_params). */
+int  mrth_bvh_cache_name(const mrth_scene* s, const mrth_build_params* p, char out[16]);
 int  mrth_bvh_build(const mrth_scene* s, const mrth_build_params* p /* NULL = defaults */, mrth_bvh** out);
 int  mrth_bvh_load(const char* datPath, mrth_bvh** out);
 int  mrth_bvh_save(const mrth_bvh* b, const char* datPath);
@@ -92,6 +102,12 @@ int  mrth_primary_rays(const mrth_camera* cam, int32_t w, int32_t h, void* rays 
 /* Primary rays sampled at (jx, jy) in [0, 1)^2 inside each pixel (centre = 0.5, 0.5). */
 int  mrth_primary_rays_subpixel(const mrth_camera* cam, int32_t w, int32_t h, float jx, float jy, void* rays,
                                 int32_t* slotToId);
+/* CameraControls::decodeSignature (CameraControls.cc:374-419, 502-554): the 6-bit text
+ * camera of the reference App's --camera argument (grtcmdline.txt). Fills cam (position,
+ * forward, up, fov, near, far) and, if non-NULL, the signature's speed and keepAligned.
+ * MRTH_ERR_INVALID_ARG for a malformed signature ("CameraControls: Invalid signature!"). */
+int  mrth_camera_decode_signature(const char* sig, mrth_camera* cam, float* speed, int32_t* keepAligned);
+
 /* invert(fitToView(-1, 2, (w, h)) * worldToClip), column-major (Renderer.cc:126-129): the
  * matrix mrt_raygen_primary (mrt.h) takes. */
 int  mrth_camera_nscreen_to_world(const mrth_camera* cam, int32_t w, int32_t h, float out[16]);
