@@ -351,7 +351,6 @@ def time_steps(launches, steps, warmup, world):
     bracketed by its own HIP event pair, the mean of which is the kernel's
     average launch duration (without inter-launch gaps)."""
     import torch
-    stream = torch.cuda.current_stream()
     warmed = warm(launches, warmup)
     torch.cuda.synchronize()
     barrier(world)
@@ -370,10 +369,11 @@ def time_steps(launches, steps, warmup, world):
     k = 0
     for _ in range(probe):
         for go in launches:
-            ev[k][0].record(stream)
+            ev[k][0].record(go.stream)
             go()
-            ev[k][1].record(stream)
+            ev[k][1].record(go.stream)
             k += 1
+            torch.cuda.synchronize()   # one launch at a time: its own duration, not an overlap
     torch.cuda.synchronize()
     per_launch = [a.elapsed_time(b) for a, b in ev]
     return wall, float(np.mean(per_launch)), warmed
@@ -526,7 +526,12 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact):
     del parts, r
     torch.cuda.synchronize()
     lo, hi = shard_range(n, world, rank)
-    launches = [tracer.launcher(big.view(a, b), exact_rcp=exact) for a, b in shard_launches(lo, hi, cfg["max_batch"])]
+    # The shard's <= 2^21-ray launches are independent batches: they alternate
+    # between two streams (each stream has its own trace scratch), so one
+    # launch's tail overlaps the next one's start.
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    spans = shard_launches(lo, hi, cfg["max_batch"])
+    launches = [tracer.launcher(big.view(a, b), exact_rcp=exact, stream=streams[i % 2]) for i, (a, b) in enumerate(spans)]
     wall, launch_ms, _ = time_steps(launches, steps, warmup, world)
     per_rank = gather_floats(wall / steps * 1e3, world)
     tn = max(per_rank)
@@ -542,7 +547,8 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact):
     if world > 1:
         equal = None
         if rank == 0:
-            one = [tracer.launcher(big.view(a, b), exact_rcp=exact) for a, b in shard_launches(0, n, cfg["max_batch"])]
+            one = [tracer.launcher(big.view(a, b), exact_rcp=exact, stream=streams[i % 2])
+                   for i, (a, b) in enumerate(shard_launches(0, n, cfg["max_batch"]))]
             w1, _, _ = time_steps(one, steps, warmup, 1)
             t1 = w1 / steps * 1e3
             equal = bool(torch.equal(full.to(big.results.device), big.results[:, :2]))
@@ -557,7 +563,7 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact):
         "eta": round(t1 / (world * tn), 4), "gather_ms": round(gather_ms, 3),
         "eta_with_gather": round(t1 / (world * (tn + gather_ms)), 4),
         "value": round(counted / (tn * 1e-3) / 1e6, 2), "value_with_gather": round(counted / ((tn + gather_ms) * 1e-3) / 1e6, 2),
-        "gathered_equals_single_gpu": equal,
+        "gathered_equals_single_gpu": equal, "streams": len(streams),
         "collective": f"{DIST_BACKEND} point-to-point gather of {n * 8} B to rank 0" if world > 1 else None,
     }
 

@@ -146,11 +146,37 @@ int variant_key(const mrt::TraceVariant& v) {
     return (v.anyHit ? 1 : 0) | (v.speculative ? 2 : 0) | (v.exactRcp ? 4 : 0) | (v.stats ? 8 : 0) | (lds << 4);
 }
 
-int grid_blocks(mrt_tracer* t, const mrt::TraceVariant& v, int numRays, int* outBlocksPerCU) {
+// The launch configuration a trace uses: the tracer's, except that with every
+// ray-distribution knob at its default a large batch over a BVH that does not fit
+// the 256 MB Infinity Cache switches to one global ray queue with refills at 48
+// live lanes and 16 waves/CU. Its rays are long (HBM-latency bound), so the
+// refill atomics are rare, and dynamic fetch evens out the per-lane sequences
+// whose static imbalance otherwise leaves half a launch with a decaying number
+// of live lanes (profiles/round2_tuning.md: hairball 1920x1080 diffuse 1.04 ->
+// 0.88 ms, primary 0.88 -> 0.73 ms). Cache-resident batches keep the static
+// strided rounds: there the same queue costs 2.6x (contended atomics).
+constexpr int64_t kMallBytes = 256ll << 20;
+constexpr int kBigBatchRaysPerLane = 4;   // of the default 20-wave grid
+constexpr int kBigQueueThreshold = 48;
+constexpr int kBigQueueWaves = 16;
+
+mrt_launch_cfg effective_cfg(const mrt_tracer* t, int numRays) {
+    mrt_launch_cfg c = t->cfg;
+    const bool defaults = c.num_queues < 0 && c.waves_per_cu == 0 && c.fetch_threshold == 0 && c.lane_groups == 1;
+    const int64_t lanes = (int64_t)std::max(1, t->numCUs) * 20 * 64;
+    if (defaults && t->nodeBytes + t->woopBytes > kMallBytes && (int64_t)numRays >= kBigBatchRaysPerLane * lanes) {
+        c.num_queues = 1;
+        c.fetch_threshold = kBigQueueThreshold;
+        c.waves_per_cu = kBigQueueWaves;
+    }
+    return c;
+}
+
+int grid_blocks(mrt_tracer* t, const mrt_launch_cfg& cfg, const mrt::TraceVariant& v, int numRays, int* outBlocksPerCU) {
     int& occ = t->occ[variant_key(v)];
     if (occ <= 0 && (mrt::trace_occupancy(v, &occ) != hipSuccess || occ <= 0)) occ = 1;
-    int waves = t->cfg.waves_per_cu;
-    if (waves == 0 && t->cfg.num_queues < 0) {
+    int waves = cfg.waves_per_cu;
+    if (waves == 0 && cfg.num_queues < 0) {
         // Static strided assignment: 28 waves/CU (7 workgroups) measured best or
         // within 2 % of best from 307k to 12.6M rays (profiles/round1_sweep.txt).
         waves = kStridedWaves;
@@ -224,7 +250,8 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     DeviceGuard guard(t->device);
     const mrt::TraceVariant v = variant_for(t, flags);
     int perCU = 0;
-    const int blocks = grid_blocks(t, v, numRays, &perCU);
+    const mrt_launch_cfg cfg = effective_cfg(t, numRays);
+    const int blocks = grid_blocks(t, cfg, v, numRays, &perCU);
     const int totalLanes = blocks * mrt::kBlockThreads;
     mrt::Workspace* ws = nullptr;
     if (int rc = workspace_for(t, stream, totalLanes, v.ldsStack, &ws)) return rc;
@@ -238,9 +265,9 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     a.nodeBytes = (uint32_t)t->nodeBytes;
     a.woopBytes = (uint32_t)t->woopBytes;
     a.numRays = numRays;
-    a.numQueues = t->cfg.num_queues < 0 ? 0 : std::min(t->cfg.num_queues, std::max(1, numRays));
-    a.fetchThreshold = t->cfg.fetch_threshold;
-    a.laneGroupsLog2 = __builtin_ctz((unsigned)t->cfg.lane_groups);
+    a.numQueues = cfg.num_queues < 0 ? 0 : std::min(cfg.num_queues, std::max(1, numRays));
+    a.fetchThreshold = cfg.fetch_threshold;
+    a.laneGroupsLog2 = __builtin_ctz((unsigned)cfg.lane_groups);
     a.totalLanes = totalLanes;
     a.queues = ws->queues;
     a.spill = ws->spill;
@@ -263,6 +290,8 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
         info->grid_waves = totalLanes / 64;
         info->block_threads = mrt::kBlockThreads;
         info->lds_stack_entries = v.ldsStack;
+        info->num_queues = a.numQueues;
+        info->fetch_threshold = a.fetchThreshold;
         int overflow = 0;
         MRT_HIP(hipMemcpy(&overflow, ws->status, sizeof(int), hipMemcpyDeviceToHost));
         info->stack_overflows = overflow;

@@ -37,7 +37,7 @@ class LaunchCfg(C.Structure):
 
 class TraceInfo(C.Structure):
     _fields_ = [("kernel_ms", f32), ("grid_waves", i32), ("block_threads", i32),
-                ("lds_stack_entries", i32), ("stack_overflows", i32)]
+                ("lds_stack_entries", i32), ("num_queues", i32), ("fetch_threshold", i32), ("stack_overflows", i32)]
 
 
 class HostCamera(C.Structure):

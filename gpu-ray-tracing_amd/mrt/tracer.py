@@ -173,6 +173,7 @@ class Tracer:
             rc = fn(h, *args)
             if rc:
                 check(rc)
+        launch.stream = stream if stream is not None else torch.cuda.current_stream()
         return launch
 
     def trace_batch(self, rays: RayBuffer, exact_rcp=False, speculative=True, stats=False, stream=None) -> float:

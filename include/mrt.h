@@ -66,7 +66,11 @@ typedef struct mrt_tracer mrt_tracer;
 
 /* Tuning knobs of the persistent launch (0 = library default). */
 typedef struct mrt_launch_cfg {
-    int32_t waves_per_cu;      /* persistent waves per CU (grid = CUs * waves_per_cu); 0 = auto (by batch size) */
+    int32_t waves_per_cu;      /* persistent waves per CU (grid = CUs * waves_per_cu); 0 = auto (by batch size).
+                                  With num_queues, waves_per_cu, fetch_threshold and lane_groups all at their
+                                  defaults, a batch of >= 4 rays per lane over a BVH larger than the 256 MB
+                                  Infinity Cache uses one global queue, refills at 48 live lanes, 16 waves/CU
+                                  (mrt_trace_info reports what a launch used) */
     int32_t fetch_threshold;   /* refill a wave when fewer than this many of its 64 lanes are live (0 = when all are done)
                                   (reference DYNAMIC_FETCH_THRESHOLD 20 of 32, kepler_dynamic_fetch.cu:48) */
     int32_t num_queues;        /* -1 (default) = static strided rounds, no atomics; 1..8 = the reference's
@@ -83,6 +87,8 @@ typedef struct mrt_trace_info {
     int32_t grid_waves;        /* persistent waves launched                                       */
     int32_t block_threads;     /* threads per workgroup                                           */
     int32_t lds_stack_entries; /* per-lane traversal-stack entries held in LDS                    */
+    int32_t num_queues;        /* ray queues the launch used (0 = static strided rounds)          */
+    int32_t fetch_threshold;   /* live-lane refill threshold the launch used                     */
     int32_t stack_overflows;   /* pushes past the 64-entry stack in this launch (then the call returns
                                   MRT_ERR_STACK_OVERFLOW; 0 for any SBVH of depth <= 64)            */
 } mrt_trace_info;

@@ -108,3 +108,26 @@ def test_strong_scaling_raybuffer_matches_the_oracle(env):
         got = b.results_numpy()
         total_bad += int(((got[:, 0] != want[:, 0]) | (got[:, 1] != want[:, 1])).sum())
     assert total_bad == 0
+
+
+@pytest.mark.parametrize("name,queues", [("hairball-diffuse-1920x1080", 1), ("hairball-diffuse-640x480", 0),
+                                         ("sponza-diffuse-640x480", 0)])
+def test_automatic_launch_config(env, name, queues):
+    """Default knobs: a batch of >= 4 rays per lane over a BVH above the 256 MB Infinity
+    Cache runs on one global queue with refills at 48 live lanes (mrt_api.cpp
+    effective_cfg); everything else on static strided rounds. Results equal the oracle
+    either way (test_baseline_config_matches_the_oracle covers both)."""
+    bench, scenes, tracer, threads = env
+    e = scenes.get(bench.workload_spec(name)[0])
+    batches = bench.Batches(name, e["scene"], e["gbvh"], tracer)
+    rb = batches.batches[0][0]
+    tracer.trace_batch(rb, exact_rcp=True)
+    assert tracer.last_info["num_queues"] == queues
+    assert tracer.last_info["fetch_threshold"] == (48 if queues else 0)
+    saved = tracer.config()
+    try:
+        tracer.set_config(waves_per_cu=20)   # any explicit distribution knob keeps the static rounds
+        tracer.trace_batch(rb, exact_rcp=True)
+        assert tracer.last_info["num_queues"] == 0
+    finally:
+        tracer.set_config(**saved)
