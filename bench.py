@@ -488,7 +488,7 @@ def run_workload(name, tracer, scenes, world, rank, steps, warmup, exact, want_c
         "bvh": {"inner_nodes": g.nodes.numel() // 16, "woop_slots": g.woop.numel() // 4, "bytes": g.total_bytes,
                 "build_s": round(e["build_s"], 2), "from_cache": e["cached"],
                 **({"max_depth": e["stats"]["max_depth"], "sah": round(e["stats"]["sah_cost"], 2)}
-                   if e["stats"] else {})},
+                   if e["stats"] and not e["cached"] else {})},
         "per_ray": {"nodes": round(n_nodes / batches.rays_traced, 2), "tris": round(n_tris / batches.rays_traced, 2),
                     "leaves": round(n_leaves / batches.rays_traced, 2),
                     "bytes": round(alg_bytes / batches.rays_traced, 1)},

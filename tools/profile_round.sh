@@ -7,7 +7,7 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 W=${1:-bunny-primary-1024x768}
 OUT=${2:-gpurun_out/prof}
-B="--workload $W --no-extra --no-cpu --bvh-cache /tmp/mrt_bvhcache"
+B="--workload $W --no-extra --no-cpu --no-strong --bvh-cache /tmp/mrt_bvhcache"
 mkdir -p $OUT
 # build (or load) the BVH once outside the profiler
 timeout -k 10 300 python3 bench.py $B --steps 2 --warmup 1 > $OUT/bench_warm.log 2>&1 || { echo "warm run failed"; tail $OUT/bench_warm.log; exit 1; }
