@@ -39,6 +39,12 @@ struct mrt_tracer {
 
     mrt_launch_cfg cfg{};
 
+    // 4-wide nodes derived from the bound Compact2 tree (cfg.wide; wide_bvh.cpp),
+    // owned by the tracer and rebuilt when the BVH or the setting changes.
+    void* wideNodes = nullptr;
+    int64_t wideBytes = 0;
+    int wideBuiltFor = -1;   // the cfg.wide value the current array was built for
+
     // Launch scratch, one set per stream the handle has launched on: the stack
     // spill slab, the queue heads and the overflow counter are written by a
     // running trace, so two traces in flight on different streams must not
@@ -48,7 +54,7 @@ struct mrt_tracer {
 
     // Occupancy per kernel variant, queried once (hipOccupancy* is a host
     // round-trip that would otherwise sit on every launch).
-    int occ[64] = {};
+    int occ[128] = {};
 
 };
 
@@ -100,6 +106,10 @@ struct DeviceGuard {
     }
 };
 
+// The production (speculative) traversal reads 4-wide nodes derived at bind time
+// (profiles/round2_tuning.md, "4-wide nodes").
+constexpr int kDefaultWide = 1;
+
 mrt_launch_cfg default_cfg() {
     mrt_launch_cfg c;
     c.waves_per_cu = 0;   // auto: sized from the batch (grid_blocks)
@@ -107,6 +117,7 @@ mrt_launch_cfg default_cfg() {
     c.num_queues = -1;       // static strided assignment (see trace_kernel.hip); 1..8 = atomic queues
     c.lds_stack = 16;
     c.lane_groups = 1;
+    c.wide = kDefaultWide;
     return c;
 }
 
@@ -114,7 +125,8 @@ bool valid_cfg(const mrt_launch_cfg& c) {
     return (c.waves_per_cu == 0 || (c.waves_per_cu >= 4 && c.waves_per_cu <= 32)) && c.fetch_threshold >= 0 && c.fetch_threshold <= 64 &&
            (c.num_queues == -1 || (c.num_queues >= 1 && c.num_queues <= mrt::kMaxQueues)) &&
            (c.lds_stack == 8 || c.lds_stack == 16 || c.lds_stack == 32) &&
-           c.lane_groups >= 1 && c.lane_groups <= 64 && (c.lane_groups & (c.lane_groups - 1)) == 0;
+           c.lane_groups >= 1 && c.lane_groups <= 64 && (c.lane_groups & (c.lane_groups - 1)) == 0 &&
+           (c.wide == 0 || c.wide == 1);
 }
 
 mrt::TraceVariant variant_for(const mrt_tracer* t, uint32_t flags) {
@@ -124,6 +136,9 @@ mrt::TraceVariant variant_for(const mrt_tracer* t, uint32_t flags) {
     v.speculative = (flags & MRT_TRACE_LOCKSTEP_OFF) == 0;
     v.stats = (flags & MRT_TRACE_STATS) != 0;
     v.ldsStack = t->cfg.lds_stack;
+    // The per-lane (lockstep-off) order is the reference's binary order: it keeps
+    // the Compact2 nodes, and with them the oracle's exact per-ray counters.
+    v.wide = t->cfg.wide == 1 && t->wideNodes != nullptr && v.speculative;
     return v;
 }
 
@@ -143,7 +158,8 @@ constexpr int kAutoMinWaves = 8;
 // workgroup is resident at once.
 int variant_key(const mrt::TraceVariant& v) {
     const int lds = v.ldsStack == 8 ? 0 : v.ldsStack == 16 ? 1 : 2;
-    return (v.anyHit ? 1 : 0) | (v.speculative ? 2 : 0) | (v.exactRcp ? 4 : 0) | (v.stats ? 8 : 0) | (lds << 4);
+    return (v.anyHit ? 1 : 0) | (v.speculative ? 2 : 0) | (v.exactRcp ? 4 : 0) | (v.stats ? 8 : 0) | (lds << 4) |
+           (v.wide ? 64 : 0);
 }
 
 // The launch configuration a trace uses: the tracer's, except that with every
@@ -228,6 +244,32 @@ int workspace_for(mrt_tracer* t, void* stream, int totalLanes, int ldsStack, mrt
     return MRT_OK;
 }
 
+// (Re)derives the 4-wide nodes of the bound BVH when cfg.wide asks for them;
+// bind, unbind and set_config call it with the handle's mutex held. Synchronous
+// (bind-time work: the Compact2 nodes come to the host, collapse, go back).
+int refresh_wide(mrt_tracer* t) {
+    const int want = t->bound ? t->cfg.wide : 0;
+    if (want == t->wideBuiltFor) return MRT_OK;
+    DeviceGuard guard(t->device);
+    MRT_HIP(hipDeviceSynchronize());   // launches in flight may still read the old array
+    if (t->wideNodes) MRT_HIP(hipFree(t->wideNodes));
+    t->wideNodes = nullptr;
+    t->wideBytes = 0;
+    t->wideBuiltFor = -1;
+    if (want) {
+        std::vector<int32_t> host((size_t)(t->nodeBytes / 4));
+        MRT_HIP(hipMemcpy(host.data(), t->nodes, (size_t)t->nodeBytes, hipMemcpyDeviceToHost));
+        const std::vector<uint32_t> wide = mrt::build_wide4(host.data(), t->nodeBytes / 64);
+        const int64_t bytes = (int64_t)wide.size() * 4;
+        if (bytes > mrt::kMaxBufferBytes) return fail(MRT_ERR_TOO_LARGE, "4-wide node array above the 32-bit range");
+        MRT_HIP(hipMalloc(&t->wideNodes, (size_t)bytes));
+        MRT_HIP(hipMemcpy(t->wideNodes, wide.data(), (size_t)bytes, hipMemcpyHostToDevice));
+        t->wideBytes = bytes;
+    }
+    t->wideBuiltFor = want;
+    return MRT_OK;
+}
+
 // Largest batch one launch takes: ray/result addressing and the strided round
 // arithmetic stay inside int32 with room for the grid (bigger batches are split
 // by the caller, as the reference Renderer does at 2^21 rays, Renderer.cc:46).
@@ -259,10 +301,10 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     mrt::TraceArgs a{};
     a.rays = static_cast<const float4*>(rays);
     a.results = static_cast<int2*>(results);
-    a.nodes = static_cast<const float4*>(t->nodes);
+    a.nodes = static_cast<const float4*>(v.wide ? t->wideNodes : t->nodes);
     a.woop = static_cast<const float4*>(t->woop);
     a.triIndex = t->triIndex;
-    a.nodeBytes = (uint32_t)t->nodeBytes;
+    a.nodeBytes = (uint32_t)(v.wide ? t->wideBytes : t->nodeBytes);
     a.woopBytes = (uint32_t)t->woopBytes;
     a.numRays = numRays;
     a.numQueues = cfg.num_queues < 0 ? 0 : std::min(cfg.num_queues, std::max(1, numRays));
@@ -290,6 +332,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
         info->grid_waves = totalLanes / 64;
         info->block_threads = mrt::kBlockThreads;
         info->lds_stack_entries = v.ldsStack;
+        info->wide = v.wide ? 4 : 2;
         info->num_queues = a.numQueues;
         info->fetch_threshold = a.fetchThreshold;
         int overflow = 0;
@@ -395,6 +438,7 @@ int mrt_tracer_destroy(mrt_tracer* t) {
     if (!t) return MRT_OK;
     {
         DeviceGuard guard(t->device);
+        if (t->wideNodes) (void)hipFree(t->wideNodes);
         for (mrt::Workspace* w : t->workspaces) {
             if (w->stream) (void)hipStreamSynchronize(static_cast<hipStream_t>(w->stream));
             if (w->queues) (void)hipFree(w->queues);
@@ -426,7 +470,8 @@ int mrt_tracer_bind(mrt_tracer* t, const void* nodes, int64_t nodeBytes, const v
     t->triIndex = triIndex;
     t->triIndexBytes = triIndexBytes;
     t->bound = true;
-    return MRT_OK;
+    t->wideBuiltFor = -1;   // a new BVH: its wide nodes are derived now (if configured)
+    return refresh_wide(t);
 }
 
 int mrt_tracer_unbind(mrt_tracer* t) {
@@ -435,7 +480,7 @@ int mrt_tracer_unbind(mrt_tracer* t) {
     t->bound = false;
     t->nodes = t->woop = nullptr;
     t->triIndex = nullptr;
-    return MRT_OK;
+    return refresh_wide(t);
 }
 
 int mrt_tracer_set_config(mrt_tracer* t, const mrt_launch_cfg* cfg) {
@@ -446,10 +491,11 @@ int mrt_tracer_set_config(mrt_tracer* t, const mrt_launch_cfg* cfg) {
     if (c.num_queues == 0) c.num_queues = d.num_queues;
     if (c.lds_stack == 0) c.lds_stack = d.lds_stack;
     if (c.lane_groups == 0) c.lane_groups = d.lane_groups;
+    if (c.wide < 0) c.wide = d.wide;   // -1 = library default
     if (!valid_cfg(c)) return fail(MRT_ERR_INVALID_ARG, "launch config out of range");
     std::lock_guard<std::mutex> lock(t->mu);
     t->cfg = c;
-    return MRT_OK;
+    return refresh_wide(t);
 }
 
 int mrt_tracer_get_config(const mrt_tracer* t, mrt_launch_cfg* cfg) {

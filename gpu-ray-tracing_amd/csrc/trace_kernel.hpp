@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <string>
+#include <vector>
 
 namespace mrt {
 
@@ -48,7 +49,12 @@ struct TraceVariant {
     bool exactRcp;      // IEEE 1/x vs v_rcp_f32
     bool stats;
     int ldsStack;       // 8, 16 or 32 LDS entries per lane
+    bool wide = false;  // the 4-wide nodes derived from the Compact2 tree (speculative mode only)
 };
+
+// The 4-wide node array derived from a Compact2 node array (numNodes inner nodes,
+// 16 int32 each): 32 uint32 (128 B) per wide node, layout in wide_bvh.cpp.
+std::vector<uint32_t> build_wide4(const int32_t* nodes, int64_t numNodes);
 
 // Launch one persistent trace. grid = number of 256-thread workgroups.
 hipError_t launch_trace(const TraceVariant& v, const TraceArgs& a, int gridBlocks, hipStream_t s);

@@ -1,0 +1,121 @@
+// wide_bvh.cpp — the 4-wide node array the production traversal reads, derived
+// at bind time from the bound Compact2 tree (CudaBVH.cc:270-357 layout).
+//
+// Collapse: every wide node starts from a binary inner node's two children and
+// repeatedly replaces its inner child of largest surface area by that child's
+// two children until it holds four (leaves stay leaves; a node may keep fewer
+// children, the rest are absent). Child boxes are the binary tree's boxes,
+// bit for bit, so the slab test of a wide child is the binary step's test of
+// that same box. Wide nodes are numbered depth first (a node's first inner child
+// follows it), 128 B each, one cache line:
+//   float4 0  (c0.lo.x, c0.hi.x, c1.lo.x, c1.hi.x)     float4 1  (c2.lo.x, c2.hi.x, c3.lo.x, c3.hi.x)
+//   float4 2  the same for y                           float4 3
+//   float4 4  the same for z                           float4 5
+//   float4 6  child refs (int): inner = float4 index of the wide node (8 per node),
+//             leaf = the Compact2 leaf ref (~woop float4 index), absent = 0x76543210
+//   float4 7  unused (zero)
+// Leaves, Woop triangles and triIndex are the Compact2 ones: the leaf loop is unchanged.
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "trace_kernel.hpp"
+
+namespace mrt {
+
+namespace {
+
+struct Child {
+    int32_t ref;
+    float lo[3], hi[3];
+};
+
+float as_float(int32_t i) {
+    float f;
+    std::memcpy(&f, &i, 4);
+    return f;
+}
+
+void binary_children(const int32_t* nodes, int32_t ref, Child out[2]) {
+    const int32_t* n = nodes + (int64_t)(ref / 4) * 16;
+    out[0] = Child{n[12], {as_float(n[0]), as_float(n[2]), as_float(n[8])}, {as_float(n[1]), as_float(n[3]), as_float(n[9])}};
+    out[1] = Child{n[13], {as_float(n[4]), as_float(n[6]), as_float(n[10])}, {as_float(n[5]), as_float(n[7]), as_float(n[11])}};
+}
+
+double half_area(const Child& c) {
+    const double x = (double)c.hi[0] - c.lo[0], y = (double)c.hi[1] - c.lo[1], z = (double)c.hi[2] - c.lo[2];
+    return x * y + y * z + z * x;
+}
+
+// The children of the wide node rooted at binary node `ref`.
+int collapse(const int32_t* nodes, int32_t ref, Child out[4]) {
+    Child two[2];
+    binary_children(nodes, ref, two);
+    out[0] = two[0];
+    out[1] = two[1];
+    int n = 2;
+    while (n < 4) {
+        int best = -1;
+        double bestArea = -1.0;
+        for (int i = 0; i < n; i++)
+            if (out[i].ref >= 0 && half_area(out[i]) > bestArea) {
+                bestArea = half_area(out[i]);
+                best = i;
+            }
+        if (best < 0) break;
+        binary_children(nodes, out[best].ref, two);
+        for (int i = n; i > best + 1; i--) out[i] = out[i - 1];   // the two grandchildren take best's place
+        out[best] = two[0];
+        out[best + 1] = two[1];
+        n++;
+    }
+    return n;
+}
+
+}  // namespace
+
+std::vector<uint32_t> build_wide4(const int32_t* nodes, int64_t numNodes) {
+    std::vector<uint32_t> out;
+    if (numNodes <= 0) return out;
+    // Pass 1: number the wide nodes depth first (binary node -> wide index).
+    std::vector<int32_t> wideOf((size_t)numNodes, -1);
+    std::vector<int32_t> order;
+    std::vector<int32_t> stack{0};
+    Child ch[4];
+    while (!stack.empty()) {
+        const int32_t ref = stack.back();
+        stack.pop_back();
+        wideOf[(size_t)(ref / 4)] = (int32_t)order.size();
+        order.push_back(ref);
+        const int n = collapse(nodes, ref, ch);
+        for (int i = n - 1; i >= 0; i--)
+            if (ch[i].ref >= 0) stack.push_back(ch[i].ref);
+    }
+    // Pass 2: write the nodes.
+    out.assign(order.size() * 32, 0u);
+    for (size_t w = 0; w < order.size(); w++) {
+        const int n = collapse(nodes, order[w], ch);
+        uint32_t* o = out.data() + w * 32;
+        for (int c = 0; c < 4; c++) {
+            const int f4 = c >> 1, pair = (c & 1) * 2;   // children 0,1 in float4 0/2/4, 2,3 in 1/3/5
+            float lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
+            int32_t ref = kEntrypointSentinel;
+            if (c < n) {
+                for (int k = 0; k < 3; k++) {
+                    lo[k] = ch[c].lo[k];
+                    hi[k] = ch[c].hi[k];
+                }
+                ref = ch[c].ref >= 0 ? wideOf[(size_t)(ch[c].ref / 4)] * 8 : ch[c].ref;
+            }
+            for (int k = 0; k < 3; k++) {
+                std::memcpy(&o[(2 * k + f4) * 4 + pair], &lo[k], 4);
+                std::memcpy(&o[(2 * k + f4) * 4 + pair + 1], &hi[k], 4);
+            }
+            o[6 * 4 + c] = (uint32_t)ref;
+        }
+    }
+    return out;
+}
+
+}  // namespace mrt

@@ -79,6 +79,11 @@ typedef struct mrt_launch_cfg {
     int32_t lds_stack;         /* traversal-stack entries per lane kept in LDS: 8, 16 or 32       */
     int32_t lane_groups;       /* strided mode: a wave's 64 lanes take rays from this many (1..64, power of
                                   two) distant sub-ranges of the batch instead of 64 consecutive rays */
+    int32_t wide;              /* 1 (default) = the speculative traversal reads 4-wide nodes derived from the
+                                  bound Compact2 tree at bind time (same child boxes, half the dependent node
+                                  fetches; closest hits equal the binary traversal's except exact-t ties);
+                                  0 = the Compact2 nodes themselves; -1 = library default. The per-lane
+                                  (MRT_TRACE_LOCKSTEP_OFF) mode always walks the Compact2 nodes */
 } mrt_launch_cfg;
 
 /* Per-launch statistics reported back to the host (optional). */
@@ -87,6 +92,7 @@ typedef struct mrt_trace_info {
     int32_t grid_waves;        /* persistent waves launched                                       */
     int32_t block_threads;     /* threads per workgroup                                           */
     int32_t lds_stack_entries; /* per-lane traversal-stack entries held in LDS                    */
+    int32_t wide;              /* node width the launch traversed: 2 (Compact2) or 4              */
     int32_t num_queues;        /* ray queues the launch used (0 = static strided rounds)          */
     int32_t fetch_threshold;   /* live-lane refill threshold the launch used                     */
     int32_t stack_overflows;   /* pushes past the 64-entry stack in this launch (then the call returns
