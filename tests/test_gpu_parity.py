@@ -240,6 +240,8 @@ def test_stack_overflow_is_reported(tracer, depth, overflow):
     from mrt import _lib
     from mrt.tracer import GpuBvh, RayBuffer
     bufs, ray, expect = kat.scene_comb(depth)
+    saved = tracer.config()
+    tracer.set_config(wide=0)   # the reference's capacity is a property of its binary traversal order
     tracer.set_bvh(GpuBvh(bufs))
     n0 = C.c_int64()
     _lib.check(tracer.lib.mrt_tracer_stack_overflows(tracer._h, C.byref(n0), 1))
@@ -261,6 +263,16 @@ def test_stack_overflow_is_reported(tracer, depth, overflow):
     assert (n.value > 0) == overflow
     _lib.check(tracer.lib.mrt_tracer_stack_overflows(tracer._h, C.byref(n), 0))
     assert n.value == 0
+    # the 4-wide traversal of the same comb pushes fewer entries: the hand answer, or a reported overflow
+    tracer.set_config(wide=1)
+    try:
+        tracer.trace_batch(rb, exact_rcp=True)
+        res = rb.results_numpy()
+        assert tracer.last_info["wide"] == 4
+        assert (res[:, 0] == expect[0]).all() and (res[:, 1] == kat.f2i(expect[1])).all()
+    except _lib.MrtError as e:
+        assert "stack overflow" in str(e)
+    tracer.set_config(**saved)
 
 
 def test_oversized_batch_rejected(tracer):
