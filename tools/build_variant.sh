@@ -10,5 +10,6 @@ HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -fgpu-flush-denormals-to-ze
 /opt/rocm/bin/hipcc $HIPFLAGS $FLAGS -c $D/csrc/trace_kernel.hip -o $B/trace_kernel.o
 /opt/rocm/bin/hipcc $HIPFLAGS $FLAGS -c $D/csrc/raygen_kernel.hip -o $B/raygen_kernel.o
 /opt/rocm/bin/hipcc $HIPFLAGS $FLAGS -x hip -c $D/csrc/mrt_api.cpp -o $B/mrt_api.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Wl,-Bsymbolic -o $OUT/libmrt.so $B/trace_kernel.o $B/raygen_kernel.o $B/mrt_api.o
+/opt/rocm/bin/hipcc $HIPFLAGS $FLAGS -x hip -c $D/csrc/wide_bvh.cpp -o $B/wide_bvh.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Wl,-Bsymbolic -o $OUT/libmrt.so $B/trace_kernel.o $B/raygen_kernel.o $B/mrt_api.o $B/wide_bvh.o
 echo "built $OUT/libmrt.so ($FLAGS)"
