@@ -150,7 +150,11 @@ mrt::TraceVariant variant_for(const mrt_tracer* t, uint32_t flags) {
 // 640x480: 0.061 ms vs 0.077 at 8 waves); above that, 8 waves/CU is best up to
 // ~1M rays (bunny primary 1024x768), 16 at 3M, 32 at 12M rays.
 constexpr int kAutoRaysPerLane = 12;
-constexpr int kStridedWaves = 28;
+// Static strided rounds: 20 waves/CU (5 per SIMD). More resident waves evict
+// each other's nodes and triangles from the vector L1 (28 waves/CU: hairball
+// -22 %, profiles/round2_tuning.md); the register budget of the 4-wide kernels
+// is sized for exactly this occupancy.
+constexpr int kStridedWaves = 20;
 constexpr int kAutoMinWaves = 8;
 
 // Persistent grid: as many 256-thread workgroups per CU as the config asks for

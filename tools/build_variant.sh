@@ -7,7 +7,7 @@ D=$(cd "$(dirname "$0")/../gpu-ray-tracing_amd" && pwd)
 OUT=$D/lib/variants/$NAME; B=/tmp/mrt_variant_$NAME
 mkdir -p $OUT $B
 HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -fgpu-flush-denormals-to-zero -ffp-contract=off -Wall -Wno-unused-result -I$D/../include"
-/opt/rocm/bin/hipcc $HIPFLAGS $FLAGS -c $D/csrc/trace_kernel.hip -o $B/trace_kernel.o
+/opt/rocm/bin/hipcc $HIPFLAGS -fno-slp-vectorize $FLAGS -c $D/csrc/trace_kernel.hip -o $B/trace_kernel.o
 /opt/rocm/bin/hipcc $HIPFLAGS $FLAGS -c $D/csrc/raygen_kernel.hip -o $B/raygen_kernel.o
 /opt/rocm/bin/hipcc $HIPFLAGS $FLAGS -x hip -c $D/csrc/mrt_api.cpp -o $B/mrt_api.o
 /opt/rocm/bin/hipcc $HIPFLAGS $FLAGS -x hip -c $D/csrc/wide_bvh.cpp -o $B/wide_bvh.o
