@@ -44,6 +44,7 @@ struct mrt_tracer {
     void* wideNodes = nullptr;
     int64_t wideBytes = 0;
     int wideBuiltFor = -1;   // the cfg.wide value the current array was built for
+    int wideFormat = mrt::kNodeCompact2;   // the form wideNodes holds (kNodeWide4 / kNodeWide4Q)
 
     // Launch scratch, one set per stream the handle has launched on: the stack
     // spill slab, the queue heads and the overflow counter are written by a
@@ -126,7 +127,7 @@ bool valid_cfg(const mrt_launch_cfg& c) {
            (c.num_queues == -1 || (c.num_queues >= 1 && c.num_queues <= mrt::kMaxQueues)) &&
            (c.lds_stack == 8 || c.lds_stack == 16 || c.lds_stack == 32) &&
            c.lane_groups >= 1 && c.lane_groups <= 64 && (c.lane_groups & (c.lane_groups - 1)) == 0 &&
-           (c.wide == 0 || c.wide == 1);
+           (c.wide >= 0 && c.wide <= 2);
 }
 
 mrt::TraceVariant variant_for(const mrt_tracer* t, uint32_t flags) {
@@ -138,7 +139,7 @@ mrt::TraceVariant variant_for(const mrt_tracer* t, uint32_t flags) {
     v.ldsStack = t->cfg.lds_stack;
     // The per-lane (lockstep-off) order is the reference's binary order: it keeps
     // the Compact2 nodes, and with them the oracle's exact per-ray counters.
-    v.wide = t->cfg.wide == 1 && t->wideNodes != nullptr && v.speculative;
+    v.nodes = (t->cfg.wide != 0 && t->wideNodes != nullptr && v.speculative) ? t->wideFormat : mrt::kNodeCompact2;
     return v;
 }
 
@@ -163,7 +164,7 @@ constexpr int kAutoMinWaves = 8;
 int variant_key(const mrt::TraceVariant& v) {
     const int lds = v.ldsStack == 8 ? 0 : v.ldsStack == 16 ? 1 : 2;
     return (v.anyHit ? 1 : 0) | (v.speculative ? 2 : 0) | (v.exactRcp ? 4 : 0) | (v.stats ? 8 : 0) | (lds << 4) |
-           (v.wide ? 64 : 0);
+           (v.nodes << 6);
 }
 
 // The launch configuration a trace uses: the tracer's, except that with every
@@ -260,15 +261,21 @@ int refresh_wide(mrt_tracer* t) {
     t->wideNodes = nullptr;
     t->wideBytes = 0;
     t->wideBuiltFor = -1;
+    t->wideFormat = mrt::kNodeCompact2;
     if (want) {
         std::vector<int32_t> host((size_t)(t->nodeBytes / 4));
         MRT_HIP(hipMemcpy(host.data(), t->nodes, (size_t)t->nodeBytes, hipMemcpyDeviceToHost));
-        const std::vector<uint32_t> wide = mrt::build_wide4(host.data(), t->nodeBytes / 64);
+        std::vector<uint32_t> wide;
+        int format = mrt::kNodeWide4;
+        // The quantized form when asked for and every box quantizes; else the exact one.
+        if (want == 2 && mrt::build_wide4q(host.data(), t->nodeBytes / 64, &wide)) format = mrt::kNodeWide4Q;
+        else wide = mrt::build_wide4(host.data(), t->nodeBytes / 64);
         const int64_t bytes = (int64_t)wide.size() * 4;
         if (bytes > mrt::kMaxBufferBytes) return fail(MRT_ERR_TOO_LARGE, "4-wide node array above the 32-bit range");
         MRT_HIP(hipMalloc(&t->wideNodes, (size_t)bytes));
         MRT_HIP(hipMemcpy(t->wideNodes, wide.data(), (size_t)bytes, hipMemcpyHostToDevice));
         t->wideBytes = bytes;
+        t->wideFormat = format;
     }
     t->wideBuiltFor = want;
     return MRT_OK;
@@ -305,10 +312,11 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     mrt::TraceArgs a{};
     a.rays = static_cast<const float4*>(rays);
     a.results = static_cast<int2*>(results);
-    a.nodes = static_cast<const float4*>(v.wide ? t->wideNodes : t->nodes);
+    const bool wide = v.nodes != mrt::kNodeCompact2;
+    a.nodes = static_cast<const float4*>(wide ? t->wideNodes : t->nodes);
     a.woop = static_cast<const float4*>(t->woop);
     a.triIndex = t->triIndex;
-    a.nodeBytes = (uint32_t)(v.wide ? t->wideBytes : t->nodeBytes);
+    a.nodeBytes = (uint32_t)(wide ? t->wideBytes : t->nodeBytes);
     a.woopBytes = (uint32_t)t->woopBytes;
     a.numRays = numRays;
     a.numQueues = cfg.num_queues < 0 ? 0 : std::min(cfg.num_queues, std::max(1, numRays));
@@ -336,7 +344,8 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
         info->grid_waves = totalLanes / 64;
         info->block_threads = mrt::kBlockThreads;
         info->lds_stack_entries = v.ldsStack;
-        info->wide = v.wide ? 4 : 2;
+        info->wide = wide ? 4 : 2;
+        info->node_bytes = v.nodes == mrt::kNodeWide4 ? 128 : 64;
         info->num_queues = a.numQueues;
         info->fetch_threshold = a.fetchThreshold;
         int overflow = 0;
@@ -532,6 +541,25 @@ int mrt_tracer_stack_overflows(mrt_tracer* t, int64_t* count, int32_t reset) {
         if (reset) MRT_HIP(hipMemset(w->status, 0, sizeof(int)));
     }
     *count = total;
+    return MRT_OK;
+}
+
+int mrt_derive_wide_nodes(const void* nodes, int64_t nodeBytes, int32_t form, void* out, int64_t outCapacity,
+                          int64_t* outBytes) {
+    if (!nodes || !outBytes || nodeBytes <= 0 || nodeBytes % 64 != 0 || (form != 1 && form != 2))
+        return fail(MRT_ERR_INVALID_ARG, "derive_wide_nodes: bad arguments");
+    std::vector<uint32_t> wide;
+    const auto* n = static_cast<const int32_t*>(nodes);
+    if (form == 2) {
+        if (!mrt::build_wide4q(n, nodeBytes / 64, &wide)) return fail(MRT_ERR_INVALID_ARG, "a box has no finite quantization");
+    } else {
+        wide = mrt::build_wide4(n, nodeBytes / 64);
+    }
+    *outBytes = (int64_t)wide.size() * 4;
+    if (out) {
+        if (outCapacity < *outBytes) return fail(MRT_ERR_TOO_LARGE, "derive_wide_nodes: output buffer too small");
+        std::memcpy(out, wide.data(), (size_t)*outBytes);
+    }
     return MRT_OK;
 }
 

@@ -42,6 +42,10 @@ struct TraceArgs {
     int4* stats;               // per-ray {nodes, tris, leaves, 0} (STATS variants)
 };
 
+// Node formats the traversal reads (wide_bvh.cpp): the bound Compact2 nodes, or
+// the 4-wide nodes derived from them at bind time, exact (128 B) or quantized (64 B).
+enum : int { kNodeCompact2 = 0, kNodeWide4 = 1, kNodeWide4Q = 2 };
+
 // Variant selector (all combinations are instantiated in trace_kernel.hip).
 struct TraceVariant {
     bool anyHit;
@@ -49,12 +53,15 @@ struct TraceVariant {
     bool exactRcp;      // IEEE 1/x vs v_rcp_f32
     bool stats;
     int ldsStack;       // 8, 16 or 32 LDS entries per lane
-    bool wide = false;  // the 4-wide nodes derived from the Compact2 tree (speculative mode only)
+    int nodes = 0;      // kNodeCompact2, or a 4-wide form derived from it (speculative mode only)
 };
 
 // The 4-wide node array derived from a Compact2 node array (numNodes inner nodes,
 // 16 int32 each): 32 uint32 (128 B) per wide node, layout in wide_bvh.cpp.
 std::vector<uint32_t> build_wide4(const int32_t* nodes, int64_t numNodes);
+// The quantized 4-wide form: 16 uint32 (64 B) per wide node. False (and no
+// output) when some child box has no finite quantization (non-finite planes).
+bool build_wide4q(const int32_t* nodes, int64_t numNodes, std::vector<uint32_t>* out);
 
 // Launch one persistent trace. grid = number of 256-thread workgroups.
 hipError_t launch_trace(const TraceVariant& v, const TraceArgs& a, int gridBlocks, hipStream_t s);

@@ -13,11 +13,30 @@
 //   float4 4  the same for z                           float4 5
 //   float4 6  child refs (int): inner = float4 index of the wide node (8 per node),
 //             leaf = the Compact2 leaf ref (~woop float4 index), absent = 0x76543210
+//             (an absent child's planes are NaN: its slab test always fails)
 //   float4 7  unused (zero)
 // Leaves, Woop triangles and triIndex are the Compact2 ones: the leaf loop is unchanged.
+//
+// The quantized form (build_wide4q) stores the same four children in 64 B, four
+// 16-B loads instead of seven (the traversal is bound by 16-B lane loads,
+// profiles/round2_tuning.md):
+//   float4 0  origin (x, y, z) = the union box's lower corner; w = three biased
+//             exponents (byte k = e_k + 127; the axis step is 2^e_k)
+//   float4 1  (qlo.x, qhi.x, qlo.y, qhi.y)  one byte per child (child c = byte c)
+//   float4 2  (qlo.z, qhi.z, 0, 0)
+//   float4 3  child refs: inner = float4 index of the wide node (4 per node),
+//             leaf = the Compact2 leaf ref, absent = 0x76543210
+// A child plane decodes as fma(q, 2^e, origin) in f32 with denormals flushed —
+// the kernel's arithmetic exactly — and q is chosen so that the decoded lower
+// plane is <= the Compact2 plane and the decoded upper plane >= it. The decoded
+// box therefore contains the binary box, its slab interval contains the binary
+// one (the slab values are monotonic in the plane), and the traversal tests a
+// superset of the leaves the binary traversal tests.
+#include <cfloat>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <limits>
 #include <vector>
 
 #include "trace_kernel.hpp"
@@ -73,14 +92,51 @@ int collapse(const int32_t* nodes, int32_t ref, Child out[4]) {
     return n;
 }
 
-}  // namespace
+// f32 with denormals flushed to (signed) zero, as the kernel computes.
+float ftz(float x) { return std::fabs(x) < FLT_MIN ? std::copysign(0.0f, x) : x; }
 
-std::vector<uint32_t> build_wide4(const int32_t* nodes, int64_t numNodes) {
-    std::vector<uint32_t> out;
-    if (numNodes <= 0) return out;
-    // Pass 1: number the wide nodes depth first (binary node -> wide index).
-    std::vector<int32_t> wideOf((size_t)numNodes, -1);
-    std::vector<int32_t> order;
+float decode(int q, float step, float origin) { return ftz(std::fmaf((float)q, step, origin)); }
+
+// Quantizes one axis of up to four children. False when no exponent fits.
+bool quantize_axis(const float* lo, const float* hi, int n, float* origin, int* biasedExp, uint8_t* qlo, uint8_t* qhi) {
+    float o = INFINITY, top = -INFINITY;
+    for (int c = 0; c < n; c++) {
+        o = std::fmin(o, ftz(lo[c]));
+        top = std::fmax(top, ftz(hi[c]));
+    }
+    if (!std::isfinite(o) || !std::isfinite(top)) return false;
+    o = ftz(o);
+    const double extent = (double)top - (double)o;
+    int e = -126;
+    if (extent > 0) e = std::max(-126, (int)std::ceil(std::log2(extent / 255.0)));
+    for (; e <= 127; e++) {
+        const float step = std::ldexp(1.0f, e);
+        bool ok = true;
+        for (int c = 0; c < n && ok; c++) {
+            const float l = ftz(lo[c]), h = ftz(hi[c]);
+            int a = (int)std::floor(((double)l - o) / step);
+            a = std::min(255, std::max(0, a));
+            while (a > 0 && decode(a, step, o) > l) a--;
+            int b = (int)std::ceil(((double)h - o) / step);
+            b = std::min(255, std::max(0, b));
+            while (b < 255 && decode(b, step, o) < h) b++;
+            if (decode(a, step, o) > l || decode(b, step, o) < h) ok = false;
+            qlo[c] = (uint8_t)a;
+            qhi[c] = (uint8_t)b;
+        }
+        if (ok) {
+            *origin = o;
+            *biasedExp = e + 127;
+            return true;
+        }
+    }
+    return false;
+}
+
+// Depth-first wide numbering: binary node -> wide index, and the binary roots in order.
+void number_wide(const int32_t* nodes, int64_t numNodes, std::vector<int32_t>& wideOf, std::vector<int32_t>& order) {
+    wideOf.assign((size_t)numNodes, -1);
+    order.clear();
     std::vector<int32_t> stack{0};
     Child ch[4];
     while (!stack.empty()) {
@@ -92,6 +148,57 @@ std::vector<uint32_t> build_wide4(const int32_t* nodes, int64_t numNodes) {
         for (int i = n - 1; i >= 0; i--)
             if (ch[i].ref >= 0) stack.push_back(ch[i].ref);
     }
+}
+
+}  // namespace
+
+bool build_wide4q(const int32_t* nodes, int64_t numNodes, std::vector<uint32_t>* out) {
+    out->clear();
+    if (numNodes <= 0) return true;
+    std::vector<int32_t> wideOf, order;
+    number_wide(nodes, numNodes, wideOf, order);
+    out->assign(order.size() * 16, 0u);
+    Child ch[4];
+    for (size_t w = 0; w < order.size(); w++) {
+        const int n = collapse(nodes, order[w], ch);
+        uint32_t* o = out->data() + w * 16;
+        uint32_t exps = 0;
+        for (int k = 0; k < 3; k++) {
+            float lo[4], hi[4], origin = 0.0f;
+            uint8_t qlo[4] = {0, 0, 0, 0}, qhi[4] = {0, 0, 0, 0};
+            int be = 0;
+            for (int c = 0; c < n; c++) {
+                lo[c] = ch[c].lo[k];
+                hi[c] = ch[c].hi[k];
+            }
+            if (!quantize_axis(lo, hi, n, &origin, &be, qlo, qhi)) return false;
+            std::memcpy(&o[k], &origin, 4);
+            exps |= (uint32_t)be << (8 * k);
+            uint32_t wl = 0, wh = 0;
+            for (int c = 0; c < 4; c++) {
+                wl |= (uint32_t)qlo[c] << (8 * c);
+                wh |= (uint32_t)qhi[c] << (8 * c);
+            }
+            o[4 + 2 * k] = wl;
+            o[5 + 2 * k] = wh;
+        }
+        o[3] = exps;
+        for (int c = 0; c < 4; c++) {
+            int32_t ref = kEntrypointSentinel;
+            if (c < n) ref = ch[c].ref >= 0 ? wideOf[(size_t)(ch[c].ref / 4)] * 4 : ch[c].ref;
+            o[12 + c] = (uint32_t)ref;
+        }
+    }
+    return true;
+}
+
+std::vector<uint32_t> build_wide4(const int32_t* nodes, int64_t numNodes) {
+    std::vector<uint32_t> out;
+    if (numNodes <= 0) return out;
+    // Pass 1: number the wide nodes depth first (binary node -> wide index).
+    std::vector<int32_t> wideOf, order;
+    number_wide(nodes, numNodes, wideOf, order);
+    Child ch[4];
     // Pass 2: write the nodes.
     out.assign(order.size() * 32, 0u);
     for (size_t w = 0; w < order.size(); w++) {
@@ -99,7 +206,9 @@ std::vector<uint32_t> build_wide4(const int32_t* nodes, int64_t numNodes) {
         uint32_t* o = out.data() + w * 32;
         for (int c = 0; c < 4; c++) {
             const int f4 = c >> 1, pair = (c & 1) * 2;   // children 0,1 in float4 0/2/4, 2,3 in 1/3/5
-            float lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
+            // an absent child: NaN planes (every slab test of it fails) and the sentinel ref
+            const float qnan = std::numeric_limits<float>::quiet_NaN();
+            float lo[3] = {qnan, qnan, qnan}, hi[3] = {qnan, qnan, qnan};
             int32_t ref = kEntrypointSentinel;
             if (c < n) {
                 for (int k = 0; k < 3; k++) {

@@ -25,6 +25,7 @@ MRT_TRACE_ANY_HIT = 1 << 0
 MRT_TRACE_EXACT_RCP = 1 << 1
 MRT_TRACE_LOCKSTEP_OFF = 1 << 2
 MRT_TRACE_STATS = 1 << 3
+MRT_ERR_INVALID_ARG = 1
 MRT_ERR_STACK_OVERFLOW = 6
 
 vp, i32, i64, u32, f32 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_float
@@ -37,7 +38,7 @@ class LaunchCfg(C.Structure):
 
 class TraceInfo(C.Structure):
     _fields_ = [("kernel_ms", f32), ("grid_waves", i32), ("block_threads", i32),
-                ("lds_stack_entries", i32), ("wide", i32), ("num_queues", i32), ("fetch_threshold", i32), ("stack_overflows", i32)]
+                ("lds_stack_entries", i32), ("wide", i32), ("num_queues", i32), ("fetch_threshold", i32), ("stack_overflows", i32), ("node_bytes", i32)]
 
 
 class HostCamera(C.Structure):
@@ -66,6 +67,7 @@ TRACE_SYMBOLS = [
     ("mrt_tracer_trace", i32, [vp, vp, vp, i32, u32, vp, vp]),
     ("mrt_tracer_trace_timed", i32, [vp, vp, vp, i32, u32, vp, vp, C.POINTER(TraceInfo)]),
     ("mrt_tracer_stack_overflows", i32, [vp, C.POINTER(i64), i32]),
+    ("mrt_derive_wide_nodes", i32, [vp, i64, i32, vp, i64, C.POINTER(i64)]),
     ("mrt_bind_bvh", i32, [vp, i64, vp, i64, vp, i64]),
     ("mrt_unbind_bvh", i32, []),
     ("mrt_trace", i32, [vp, vp, i32, i32, vp, C.POINTER(f32)]),

@@ -79,10 +79,13 @@ typedef struct mrt_launch_cfg {
     int32_t lds_stack;         /* traversal-stack entries per lane kept in LDS: 8, 16 or 32       */
     int32_t lane_groups;       /* strided mode: a wave's 64 lanes take rays from this many (1..64, power of
                                   two) distant sub-ranges of the batch instead of 64 consecutive rays */
-    int32_t wide;              /* 1 (default) = the speculative traversal reads 4-wide nodes derived from the
-                                  bound Compact2 tree at bind time (same child boxes, half the dependent node
-                                  fetches; closest hits equal the binary traversal's except exact-t ties);
-                                  0 = the Compact2 nodes themselves; -1 = library default. The per-lane
+    int32_t wide;              /* the speculative traversal reads 4-wide nodes derived from the bound
+                                  Compact2 tree at bind time (half the dependent node fetches; closest hits
+                                  equal the binary traversal's except exact-t ties): 1 = exact child boxes
+                                  (128-B nodes), 2 = child boxes quantized outward to 8 bits per plane
+                                  (64-B nodes; a superset of the binary traversal's leaves, falls back to 1
+                                  when a box has no finite quantization); 0 = the Compact2 nodes
+                                  themselves; -1 = library default. The per-lane
                                   (MRT_TRACE_LOCKSTEP_OFF) mode always walks the Compact2 nodes */
 } mrt_launch_cfg;
 
@@ -97,6 +100,7 @@ typedef struct mrt_trace_info {
     int32_t fetch_threshold;   /* live-lane refill threshold the launch used                     */
     int32_t stack_overflows;   /* pushes past the 64-entry stack in this launch (then the call returns
                                   MRT_ERR_STACK_OVERFLOW; 0 for any SBVH of depth <= 64)            */
+    int32_t node_bytes;        /* bytes per node the launch read: 64 (Compact2 or quantized 4-wide), 128 */
 } mrt_trace_info;
 
 /* ---- handle API -------------------------------------------------------- */
@@ -133,6 +137,15 @@ int  mrt_tracer_trace_timed(mrt_tracer* t, const void* rays, void* results, int3
 /* Stack overflows of asynchronous launches since the last reset, summed over the
  * handle's streams (synchronises them). reset != 0 zeroes the counters. */
 int  mrt_tracer_stack_overflows(mrt_tracer* t, int64_t* count, int32_t reset);
+
+/* Host-only (no device): the 4-wide node array a tracer derives at bind time
+ * from a Compact2 node array (host memory). form 1 = exact child boxes, 128 B per
+ * node; form 2 = child boxes quantized outward, 64 B per node (layouts in
+ * csrc/wide_bvh.cpp). *outBytes = the array's size; it is copied to out when
+ * out != NULL and outCapacity suffices (else MRT_ERR_TOO_LARGE). Form 2 returns
+ * MRT_ERR_INVALID_ARG when some box has no finite quantization. */
+int  mrt_derive_wide_nodes(const void* nodes, int64_t nodeBytes, int32_t form, void* out, int64_t outCapacity,
+                           int64_t* outBytes);
 
 /* Diagnostics: run the EXACT variants' reciprocal (v_rcp_f32 + one FMA Newton step)
  * against the correctly rounded 1.0f / x for all 2^32 inputs on the current device;
