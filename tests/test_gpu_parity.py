@@ -146,6 +146,36 @@ def test_exact_speculative(tracer, wl):
 
 
 @pytest.mark.parametrize("wl", WORKLOADS, ids=lambda w: "-".join(map(str, w)))
+def test_quantized_wide_nodes(tracer, wl):
+    """cfg.wide=2: the 64-B nodes' boxes contain the binary boxes, so the traversal
+    tests a superset of the binary traversal's leaves. Closest hits equal the
+    oracle's except where that superset holds a hit the oracle's own slab test
+    rejected at a box boundary (a grazing ray; ~1 in 10^5-10^6 rays): such a hit
+    must be a genuine Woop hit no farther than the oracle's. Any-hit results are
+    genuine hits with the oracle's hit/miss outcome."""
+    bufs, rays, any_hit, want, _ = scene_setup(*wl)
+    saved = tracer.config()
+    try:
+        tracer.set_config(wide=2)
+        res, _ = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=True)
+        assert tracer.last_info["node_bytes"] == 64 and tracer.last_info["wide"] == 4
+    finally:
+        tracer.set_config(**saved)
+    if any_hit:
+        assert_valid_hits(rays, res, want, bufs)
+        return
+    diff = np.nonzero((res[:, 0] != want[:, 0]) | (res[:, 1] != want[:, 1]))[0]
+    assert len(diff) <= max(2, len(rays) // 10000), f"{len(diff)} rays differ"
+    closer = res[diff, 1].view(np.float32) <= want[diff, 1].view(np.float32)
+    assert closer.all() and (res[diff, 0] != -1).all(), "a quantized-node hit is farther than the oracle's"
+    nodes, woop, tri = bufs
+    woop4 = woop.reshape(-1, 4)
+    for i in diff:
+        cand = np.nonzero((tri == res[i, 0]) & (woop4[:, 0] != np.int32(-2147483648)))[0]
+        assert any(O.woop_hit(rays[i], woop, s, float(rays[i][7]))[0] for s in cand), f"ray {i}: not a Woop hit"
+
+
+@pytest.mark.parametrize("wl", WORKLOADS, ids=lambda w: "-".join(map(str, w)))
 def test_fast_rcp_within_tolerance(tracer, wl):
     bufs, rays, any_hit, want, _ = scene_setup(*wl)
     res, _ = gpu_trace(tracer, bufs, rays, any_hit, exact=False, spec=True)
