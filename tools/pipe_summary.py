@@ -41,8 +41,9 @@ def main():
                   "SQ_ACTIVE_INST_VMEM", "SQ_ACTIVE_INST_VALU"):
             if k in c:
                 print(f"{k:40s} / SQ_WAVE_CYCLES {c[k] / c['SQ_WAVE_CYCLES']:8.3f}")
-        if "SQ_INST_LEVEL_VMEM" in c and "SQ_INSTS_VMEM_RD" in c:
-            print(f"mean vmem latency (INST_LEVEL_VMEM / INSTS_VMEM_RD) {c['SQ_INST_LEVEL_VMEM'] / c['SQ_INSTS_VMEM_RD']:8.1f} cycles")
+    if "SQ_INSTS_VALU" in c and "GRBM_GUI_ACTIVE" in c:
+        # a wave64 VALU op occupies a 16-lane SIMD 4 cycles; 4 SIMDs per CU
+        print(f"VALU busy (INSTS_VALU x 4 cycles / SIMD cycles)  {c['SQ_INSTS_VALU'] * 4 / (cus * 4) / cyc:.3f}")
     if "SQ_THREAD_CYCLES_VALU" in c and "SQ_ACTIVE_INST_VALU" in c:
         print(f"VALU lane utilisation (THREAD_CYCLES / 64 / ACTIVE_INST) {c['SQ_THREAD_CYCLES_VALU'] / 64 / c['SQ_ACTIVE_INST_VALU']:.3f}")
 
