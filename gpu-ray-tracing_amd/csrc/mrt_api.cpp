@@ -110,6 +110,11 @@ struct DeviceGuard {
 // The production (speculative) traversal reads 4-wide nodes derived at bind time
 // (profiles/round2_tuning.md, "4-wide nodes").
 constexpr int kDefaultWide = 1;
+// The speculative traversal turns to its leaves once at most two lanes of the
+// wave still search for one, instead of waiting for the last lane (reference
+// kepler_dynamic_fetch.cu:300-315): +3...+9 % on primary, diffuse and AO batches,
+// -3 % on AO 1280x960 (profiles/round2_tuning.md).
+constexpr int kDefaultSpecSlack = 2;
 
 mrt_launch_cfg default_cfg() {
     mrt_launch_cfg c;
@@ -119,6 +124,7 @@ mrt_launch_cfg default_cfg() {
     c.lds_stack = 16;
     c.lane_groups = 1;
     c.wide = kDefaultWide;
+    c.spec_slack = kDefaultSpecSlack;
     return c;
 }
 
@@ -127,7 +133,7 @@ bool valid_cfg(const mrt_launch_cfg& c) {
            (c.num_queues == -1 || (c.num_queues >= 1 && c.num_queues <= mrt::kMaxQueues)) &&
            (c.lds_stack == 8 || c.lds_stack == 16 || c.lds_stack == 32) &&
            c.lane_groups >= 1 && c.lane_groups <= 64 && (c.lane_groups & (c.lane_groups - 1)) == 0 &&
-           (c.wide >= 0 && c.wide <= 2);
+           (c.wide >= 0 && c.wide <= 2) && c.spec_slack >= 0 && c.spec_slack <= 63;
 }
 
 mrt::TraceVariant variant_for(const mrt_tracer* t, uint32_t flags) {
@@ -212,7 +218,8 @@ int grid_blocks(mrt_tracer* t, const mrt_launch_cfg& cfg, const mrt::TraceVarian
             waves = (int)std::min<long long>(32, std::max<long long>(kAutoMinWaves, (lanesPerCU + 63) / 64));
         }
     }
-    const int want = std::max(1, (waves + 3) / (mrt::kBlockThreads / 64));
+    constexpr int wavesPerBlock = mrt::kBlockThreads / 64;
+    const int want = std::max(1, (waves + wavesPerBlock - 1) / wavesPerBlock);
     const int perCU = std::min(want, occ);
     if (outBlocksPerCU) *outBlocksPerCU = perCU;
     return perCU * t->numCUs;
@@ -321,6 +328,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     a.numRays = numRays;
     a.numQueues = cfg.num_queues < 0 ? 0 : std::min(cfg.num_queues, std::max(1, numRays));
     a.fetchThreshold = cfg.fetch_threshold;
+    a.specSlack = cfg.spec_slack;
     a.laneGroupsLog2 = __builtin_ctz((unsigned)cfg.lane_groups);
     a.totalLanes = totalLanes;
     a.queues = ws->queues;
@@ -505,6 +513,7 @@ int mrt_tracer_set_config(mrt_tracer* t, const mrt_launch_cfg* cfg) {
     if (c.lds_stack == 0) c.lds_stack = d.lds_stack;
     if (c.lane_groups == 0) c.lane_groups = d.lane_groups;
     if (c.wide < 0) c.wide = d.wide;   // -1 = library default
+    if (c.spec_slack < 0) c.spec_slack = d.spec_slack;
     if (!valid_cfg(c)) return fail(MRT_ERR_INVALID_ARG, "launch config out of range");
     std::lock_guard<std::mutex> lock(t->mu);
     t->cfg = c;

@@ -18,7 +18,10 @@ constexpr int kEntrypointSentinel = 0x76543210;
 constexpr int kStackCapacity = 64;
 constexpr int kMaxQueues = 8;
 constexpr int kQueueStrideWords = 64;      // one 256-B line per queue head
-constexpr int kBlockThreads = 256;         // 4 wave64s per workgroup
+#ifndef MRT_BLOCK_THREADS
+#define MRT_BLOCK_THREADS 256
+#endif
+constexpr int kBlockThreads = MRT_BLOCK_THREADS;   // wave64s per workgroup x 64 (default 4 waves)
 // Largest node / woop buffer a tracer binds (32-bit buffer offsets).
 constexpr int64_t kMaxBufferBytes = 0xFFFFFFC0ll;
 
@@ -34,6 +37,7 @@ struct TraceArgs {
     int numRays;
     int numQueues;             // 1..8 ray queues (per-XCD heads)
     int fetchThreshold;        // refill when fewer live lanes than this
+    int specSlack;             // speculative: leave the node loop once <= this many lanes lack a leaf
     int laneGroupsLog2;        // strided mode: a wave's lanes take rays from 2^k spread-out sub-ranges
     int totalLanes;            // grid lanes (stride of the spill slab)
     unsigned* queues;          // numQueues heads, kQueueStrideWords apart, zeroed per launch

@@ -87,6 +87,9 @@ typedef struct mrt_launch_cfg {
                                   when a box has no finite quantization); 0 = the Compact2 nodes
                                   themselves; -1 = library default. The per-lane
                                   (MRT_TRACE_LOCKSTEP_OFF) mode always walks the Compact2 nodes */
+    int32_t spec_slack;        /* speculative mode: a wave turns from its inner nodes to its postponed leaves
+                                  once at most this many of its lanes are still without a leaf (0..63; the
+                                  reference waits for all, i.e. 0; default 2; -1 = library default) */
 } mrt_launch_cfg;
 
 /* Per-launch statistics reported back to the host (optional). */

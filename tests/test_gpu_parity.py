@@ -206,7 +206,8 @@ def test_exact_reciprocal_is_correctly_rounded_for_every_float(tracer):
                                  dict(waves_per_cu=4, lds_stack=8, num_queues=3),
                                  dict(lds_stack=32, waves_per_cu=4, fetch_threshold=48),
                                  dict(num_queues=1, fetch_threshold=48, waves_per_cu=16), dict(lane_groups=2),
-                                 dict(lane_groups=8), dict(lane_groups=64, waves_per_cu=4)],
+                                 dict(lane_groups=8), dict(lane_groups=64, waves_per_cu=4), dict(spec_slack=0),
+                                 dict(spec_slack=63), dict(spec_slack=7, num_queues=2, fetch_threshold=40)],
                          ids=lambda c: ",".join(f"{k}={v}" for k, v in c.items()))
 def test_launch_configs_do_not_change_results(tracer, cfg):
     bufs, rays, any_hit, want, st = scene_setup("conference", 256, 192, "diffuse")
@@ -323,6 +324,10 @@ def test_invalid_config_rejected(tracer):
         tracer.set_config(num_queues=9)
     with pytest.raises(MrtError):
         tracer.set_config(lane_groups=3)
+    with pytest.raises(MrtError):
+        tracer.set_config(spec_slack=64)
+    with pytest.raises(MrtError):
+        tracer.set_config(wide=3)
 
 
 # ---------------------------------------------------------------- edge cases
