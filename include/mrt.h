@@ -68,7 +68,7 @@ typedef struct mrt_tracer mrt_tracer;
 typedef struct mrt_launch_cfg {
     int32_t waves_per_cu;      /* persistent waves per CU (grid = CUs * waves_per_cu); 0 = auto (by batch size).
                                   With num_queues, waves_per_cu, fetch_threshold and lane_groups all at their
-                                  defaults, a batch of >= 4 rays per lane over a BVH larger than the 256 MB
+                                  defaults, a batch of > 1 ray per lane over a BVH larger than the 256 MB
                                   Infinity Cache uses one global queue, refills at 48 live lanes, 16 waves/CU
                                   (mrt_trace_info reports what a launch used) */
     int32_t fetch_threshold;   /* refill a wave when fewer than this many of its 64 lanes are live (0 = when all are done)

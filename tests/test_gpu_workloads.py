@@ -110,10 +110,11 @@ def test_strong_scaling_raybuffer_matches_the_oracle(env):
     assert total_bad == 0
 
 
-@pytest.mark.parametrize("name,queues", [("hairball-diffuse-1920x1080", 1), ("hairball-diffuse-640x480", 0),
-                                         ("sponza-diffuse-640x480", 0)])
+@pytest.mark.parametrize("name,queues", [("hairball-diffuse-1920x1080", 1), ("hairball-primary-1024x768", 1),
+                                         ("hairball-diffuse-640x480", 0), ("sponza-diffuse-640x480", 0),
+                                         ("bunny-primary-1024x768", 0)])
 def test_automatic_launch_config(env, name, queues):
-    """Default knobs: a batch of >= 4 rays per lane over a BVH above the 256 MB Infinity
+    """Default knobs: a batch of > 1 ray per lane over a BVH above the 256 MB Infinity
     Cache runs on one global queue with refills at 48 live lanes (mrt_api.cpp
     effective_cfg); everything else on static strided rounds. Results equal the oracle
     either way (test_baseline_config_matches_the_oracle covers both)."""
