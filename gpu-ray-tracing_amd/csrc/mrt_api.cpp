@@ -174,29 +174,30 @@ int variant_key(const mrt::TraceVariant& v) {
 }
 
 // The launch configuration a trace uses: the tracer's, except that with every
-// ray-distribution knob at its default a batch of more than one ray per lane
-// over a BVH that does not fit the 256 MB Infinity Cache switches to one global
-// ray queue with refills at 48 live lanes and 16 waves/CU. Its rays are long
-// (HBM-latency bound), so the refill atomics are rare, and dynamic fetch evens
-// out the per-lane sequences whose static imbalance otherwise leaves much of a
-// launch with a decaying number of live lanes (profiles/round2_tuning.md:
-// hairball diffuse 1920x1080 1.04 -> 0.88 ms, primary 1024x768 0.72 -> 0.43 ms,
-// diffuse 1280x960 0.89 -> 0.65 ms). A batch of at most one ray per lane is one
-// static round either way. Cache-resident batches keep the static strided
+// ray-distribution knob at its default a batch over a BVH that does not fit the
+// 256 MB Infinity Cache runs on one global ray queue with refills at 48 live
+// lanes. Its rays are long (HBM-latency bound), so the refill atomics are rare,
+// and dynamic fetch evens out the per-lane sequences whose static imbalance
+// otherwise leaves much of a launch with a decaying number of live lanes. Small
+// batches (at most 3 rays per lane of a 16-wave grid) get 12 waves/CU, so that even
+// they refill; larger ones 16. Measured (profiles/round2_tuning.md): hairball
+// diffuse 640x480 0.365 -> 0.301 ms, primary 1024x768 0.72 -> 0.42 ms, diffuse
+// 1920x1080 1.04 -> 0.82 ms. Cache-resident batches keep the static strided
 // rounds: there the same queue costs up to 2.6x (contended atomics).
 constexpr int64_t kMallBytes = 256ll << 20;
-constexpr int kBigBatchRaysPerLane = 1;   // more than this many rays per lane of the default 20-wave grid
 constexpr int kBigQueueThreshold = 48;
 constexpr int kBigQueueWaves = 16;
+constexpr int kBigQueueWavesSmall = 12;
+constexpr int kBigQueueSmallRaysPerLane = 3;   // of the 16-wave grid
 
 mrt_launch_cfg effective_cfg(const mrt_tracer* t, int numRays) {
     mrt_launch_cfg c = t->cfg;
     const bool defaults = c.num_queues < 0 && c.waves_per_cu == 0 && c.fetch_threshold == 0 && c.lane_groups == 1;
-    const int64_t lanes = (int64_t)std::max(1, t->numCUs) * 20 * 64;
-    if (defaults && t->nodeBytes + t->woopBytes > kMallBytes && (int64_t)numRays > kBigBatchRaysPerLane * lanes) {
+    if (defaults && t->nodeBytes + t->woopBytes > kMallBytes) {
+        const int64_t lanes16 = (int64_t)std::max(1, t->numCUs) * kBigQueueWaves * 64;
         c.num_queues = 1;
         c.fetch_threshold = kBigQueueThreshold;
-        c.waves_per_cu = kBigQueueWaves;
+        c.waves_per_cu = (int64_t)numRays <= kBigQueueSmallRaysPerLane * lanes16 ? kBigQueueWavesSmall : kBigQueueWaves;
     }
     return c;
 }

@@ -68,9 +68,9 @@ typedef struct mrt_tracer mrt_tracer;
 typedef struct mrt_launch_cfg {
     int32_t waves_per_cu;      /* persistent waves per CU (grid = CUs * waves_per_cu); 0 = auto (by batch size).
                                   With num_queues, waves_per_cu, fetch_threshold and lane_groups all at their
-                                  defaults, a batch of > 1 ray per lane over a BVH larger than the 256 MB
-                                  Infinity Cache uses one global queue, refills at 48 live lanes, 16 waves/CU
-                                  (mrt_trace_info reports what a launch used) */
+                                  defaults, a batch over a BVH larger than the 256 MB Infinity Cache uses
+                                  one global queue, refills at 48 live lanes, 12 waves/CU up to 3 rays per
+                                  lane of a 16-wave grid, else 16 (mrt_trace_info reports what a launch used) */
     int32_t fetch_threshold;   /* refill a wave when fewer than this many of its 64 lanes are live (0 = when all are done)
                                   (reference DYNAMIC_FETCH_THRESHOLD 20 of 32, kepler_dynamic_fetch.cu:48) */
     int32_t num_queues;        /* -1 (default) = static strided rounds, no atomics; 1..8 = the reference's

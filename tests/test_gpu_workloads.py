@@ -110,14 +110,15 @@ def test_strong_scaling_raybuffer_matches_the_oracle(env):
     assert total_bad == 0
 
 
-@pytest.mark.parametrize("name,queues", [("hairball-diffuse-1920x1080", 1), ("hairball-primary-1024x768", 1),
-                                         ("hairball-diffuse-640x480", 0), ("sponza-diffuse-640x480", 0),
-                                         ("bunny-primary-1024x768", 0)])
-def test_automatic_launch_config(env, name, queues):
-    """Default knobs: a batch of > 1 ray per lane over a BVH above the 256 MB Infinity
-    Cache runs on one global queue with refills at 48 live lanes (mrt_api.cpp
-    effective_cfg); everything else on static strided rounds. Results equal the oracle
-    either way (test_baseline_config_matches_the_oracle covers both)."""
+@pytest.mark.parametrize("name,queues,waves", [("hairball-diffuse-1920x1080", 1, 16), ("hairball-primary-1024x768", 1, 12),
+                                               ("hairball-diffuse-640x480", 1, 12), ("sponza-diffuse-640x480", 0, 20),
+                                               ("bunny-primary-1024x768", 0, 20)])
+def test_automatic_launch_config(env, name, queues, waves):
+    """Default knobs: a batch over a BVH above the 256 MB Infinity Cache runs on one
+    global queue with refills at 48 live lanes, 12 waves/CU up to 3 rays per lane of a
+    16-wave grid, else 16 (mrt_api.cpp effective_cfg); everything else on static
+    strided rounds at 20 waves/CU. Results equal the oracle either way
+    (test_baseline_config_matches_the_oracle covers both)."""
     bench, scenes, tracer, threads = env
     e = scenes.get(bench.workload_spec(name)[0])
     batches = bench.Batches(name, e["scene"], e["gbvh"], tracer)
@@ -125,6 +126,7 @@ def test_automatic_launch_config(env, name, queues):
     tracer.trace_batch(rb, exact_rcp=True)
     assert tracer.last_info["num_queues"] == queues
     assert tracer.last_info["fetch_threshold"] == (48 if queues else 0)
+    assert tracer.last_info["grid_waves"] == waves * torch.cuda.get_device_properties(0).multi_processor_count
     saved = tracer.config()
     try:
         tracer.set_config(waves_per_cu=20)   # any explicit distribution knob keeps the static rounds
