@@ -125,6 +125,7 @@ mrt_launch_cfg default_cfg() {
     c.lane_groups = 1;
     c.wide = kDefaultWide;
     c.spec_slack = kDefaultSpecSlack;
+    c.static_rounds = 1;
     return c;
 }
 
@@ -133,7 +134,8 @@ bool valid_cfg(const mrt_launch_cfg& c) {
            (c.num_queues == -1 || (c.num_queues >= 1 && c.num_queues <= mrt::kMaxQueues)) &&
            (c.lds_stack == 8 || c.lds_stack == 16 || c.lds_stack == 32) &&
            c.lane_groups >= 1 && c.lane_groups <= 64 && (c.lane_groups & (c.lane_groups - 1)) == 0 &&
-           (c.wide >= 0 && c.wide <= 2) && c.spec_slack >= 0 && c.spec_slack <= 63;
+           (c.wide >= 0 && c.wide <= 2) && c.spec_slack >= 0 && c.spec_slack <= 63 &&
+           c.static_rounds >= 1 && c.static_rounds <= 64;
 }
 
 mrt::TraceVariant variant_for(const mrt_tracer* t, uint32_t flags) {
@@ -332,6 +334,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     a.numQueues = cfg.num_queues < 0 ? 0 : std::min(cfg.num_queues, std::max(1, numRays));
     a.fetchThreshold = cfg.fetch_threshold;
     a.specSlack = cfg.spec_slack;
+    a.staticRounds = cfg.static_rounds;
     a.laneGroupsLog2 = __builtin_ctz((unsigned)cfg.lane_groups);
     a.totalLanes = totalLanes;
     a.queues = ws->queues;
@@ -517,6 +520,7 @@ int mrt_tracer_set_config(mrt_tracer* t, const mrt_launch_cfg* cfg) {
     if (c.lane_groups == 0) c.lane_groups = d.lane_groups;
     if (c.wide < 0) c.wide = d.wide;   // -1 = library default
     if (c.spec_slack < 0) c.spec_slack = d.spec_slack;
+    if (c.static_rounds == 0) c.static_rounds = d.static_rounds;
     if (!valid_cfg(c)) return fail(MRT_ERR_INVALID_ARG, "launch config out of range");
     std::lock_guard<std::mutex> lock(t->mu);
     t->cfg = c;

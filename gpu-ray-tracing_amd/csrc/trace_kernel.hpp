@@ -38,6 +38,7 @@ struct TraceArgs {
     int numQueues;             // 1..8 ray queues (per-XCD heads)
     int fetchThreshold;        // refill when fewer live lanes than this
     int specSlack;             // speculative: leave the node loop once <= this many lanes lack a leaf
+    int staticRounds;          // queue modes: static strided rounds of the grid before the queues
     int laneGroupsLog2;        // strided mode: a wave's lanes take rays from 2^k spread-out sub-ranges
     int totalLanes;            // grid lanes (stride of the spill slab)
     unsigned* queues;          // numQueues heads, kQueueStrideWords apart, zeroed per launch

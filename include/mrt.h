@@ -90,6 +90,8 @@ typedef struct mrt_launch_cfg {
     int32_t spec_slack;        /* speculative mode: a wave turns from its inner nodes to its postponed leaves
                                   once at most this many of its lanes are still without a leaf (0..63; the
                                   reference waits for all, i.e. 0; default 2; -1 = library default) */
+    int32_t static_rounds;     /* queue modes (num_queues >= 1): rays handed out in this many static strided
+                                  rounds of the grid before the queues take over (1..64; 0 = default 1) */
 } mrt_launch_cfg;
 
 /* Per-launch statistics reported back to the host (optional). */
