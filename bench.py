@@ -593,6 +593,7 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (RCCL) for real runs; gloo only to rehearse N>1 ranks on one GPU")
     ap.add_argument("--lane-groups", type=int, default=0)
+    ap.add_argument("--no-autotune", action="store_true", help="the fixed schedule rule instead of per-size autotuning")
     args = ap.parse_args()
 
     from mrt.tracer import Tracer
@@ -610,6 +611,8 @@ def main():
         cfg["num_queues"] = args.queues
     if args.lane_groups:
         cfg["lane_groups"] = args.lane_groups
+    if args.no_autotune:
+        cfg["autotune"] = 0
     if cfg:
         tracer.set_config(**cfg)
     exact = args.rcp == "exact"

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -57,6 +58,28 @@ struct mrt_tracer {
     // round-trip that would otherwise sit on every launch).
     int occ[128] = {};
 
+    // cfg.autotune: per (batch size, variant) the ray-distribution schedule the
+    // measured launches chose (mrt_api.cpp autotune_*), reset on bind/set_config.
+    std::map<std::pair<int, int>, struct TuneState*> tunes;
+};
+
+// Launch-schedule autotuning state of one (batch size, kernel variant).
+struct TuneState {
+    static constexpr int kCandidates = 5;
+    static constexpr int kSamples = 3;   // timed launches per candidate (the minimum counts)
+    float best[kCandidates];
+    int samples[kCandidates] = {};
+    int next = 0;        // candidate the next exploring launch uses
+    int locked = -1;     // the chosen candidate, once every one has kSamples samples
+    void* stream = nullptr;          // the stream this batch size was first launched on
+    bool multiStream = false;        // launched on several streams: keeps the fixed rule
+    struct Pending {
+        hipEvent_t start = nullptr, stop = nullptr;
+        int cand = -1;   // -1 = slot free
+    } pending[16];   // launches in flight with a timing (back-to-back launches complete later)
+    TuneState() {
+        for (float& b : best) b = 1e30f;
+    }
 };
 
 namespace mrt {
@@ -115,6 +138,9 @@ constexpr int kDefaultWide = 1;
 // kepler_dynamic_fetch.cu:300-315): +3...+9 % on primary, diffuse and AO batches,
 // -3 % on AO 1280x960 (profiles/round2_tuning.md).
 constexpr int kDefaultSpecSlack = 2;
+// Launch schedules are tuned per batch size (autotune_*, below): equal or faster on
+// every workload once settled (+9...+16 % on bunny/dragon primary batches).
+constexpr int kDefaultAutotune = 1;
 
 mrt_launch_cfg default_cfg() {
     mrt_launch_cfg c;
@@ -126,6 +152,7 @@ mrt_launch_cfg default_cfg() {
     c.wide = kDefaultWide;
     c.spec_slack = kDefaultSpecSlack;
     c.static_rounds = 1;
+    c.autotune = kDefaultAutotune;
     return c;
 }
 
@@ -135,7 +162,7 @@ bool valid_cfg(const mrt_launch_cfg& c) {
            (c.lds_stack == 8 || c.lds_stack == 16 || c.lds_stack == 32) &&
            c.lane_groups >= 1 && c.lane_groups <= 64 && (c.lane_groups & (c.lane_groups - 1)) == 0 &&
            (c.wide >= 0 && c.wide <= 2) && c.spec_slack >= 0 && c.spec_slack <= 63 &&
-           c.static_rounds >= 1 && c.static_rounds <= 64;
+           c.static_rounds >= 1 && c.static_rounds <= 64 && (c.autotune == 0 || c.autotune == 1);
 }
 
 mrt::TraceVariant variant_for(const mrt_tracer* t, uint32_t flags) {
@@ -293,6 +320,64 @@ int refresh_wide(mrt_tracer* t) {
     return MRT_OK;
 }
 
+// ---- launch-schedule autotuning (cfg.autotune) ---------------------------------
+// The ray-distribution schedule that wins depends on the frame: on how the
+// expensive rays fall on the static rounds, on the ray length and on the BVH's
+// cache residency (profiles/round2_tuning.md: static rounds, fewer waves, per-XCD
+// queues and the global queue each win somewhere by 5-70 %). With cfg.autotune
+// and the distribution knobs at their defaults, the first launches of a batch
+// size cycle through these candidates, each timed with an event pair that is
+// read back on a later launch (never blocking), and after kSamples launches each
+// the fastest is kept for that batch size. Results do not depend on the schedule
+// (closest hits are the same hits; an any-hit ray may report a different valid hit).
+constexpr int kMaxTuned = 64;   // batch sizes tuned per handle; others use the rule
+
+mrt_launch_cfg tune_candidate(const mrt_launch_cfg& base, int c) {
+    mrt_launch_cfg x = base;
+    x.fetch_threshold = 0;
+    x.waves_per_cu = 0;
+    x.num_queues = -1;
+    switch (c) {
+        case 0: break;                                                      // static rounds, 20 waves/CU
+        case 1: x.waves_per_cu = 8; break;                                  // static rounds, 8 waves/CU
+        case 2: x.num_queues = 8; break;                                    // per-XCD queues
+        case 3: x.num_queues = 1; x.fetch_threshold = 48; x.waves_per_cu = 16; break;   // global queue
+        default: x.num_queues = 1; x.fetch_threshold = 48; x.waves_per_cu = 12; break;
+    }
+    return x;
+}
+
+void tune_collect(TuneState* st) {
+    for (auto& p : st->pending) {
+        if (p.cand < 0 || hipEventQuery(p.stop) != hipSuccess) continue;
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, p.start, p.stop) == hipSuccess) {
+            st->best[p.cand] = std::min(st->best[p.cand], ms);
+            st->samples[p.cand]++;
+        }
+        p.cand = -1;
+    }
+    if (st->locked >= 0) return;
+    for (int c = 0; c < TuneState::kCandidates; c++)
+        if (st->samples[c] < TuneState::kSamples) return;
+    int best = 0;
+    for (int c = 1; c < TuneState::kCandidates; c++)
+        if (st->best[c] < st->best[best]) best = c;
+    st->locked = best;
+}
+
+void tune_reset(mrt_tracer* t) {
+    for (auto& kv : t->tunes) {
+        for (auto& p : kv.second->pending) {
+            if (p.start) (void)hipEventSynchronize(p.stop);
+            if (p.start) (void)hipEventDestroy(p.start);
+            if (p.stop) (void)hipEventDestroy(p.stop);
+        }
+        delete kv.second;
+    }
+    t->tunes.clear();
+}
+
 // Largest batch one launch takes: ray/result addressing and the strided round
 // arithmetic stay inside int32 with room for the grid (bigger batches are split
 // by the caller, as the reference Renderer does at 2^21 rays, Renderer.cc:46).
@@ -315,7 +400,48 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     DeviceGuard guard(t->device);
     const mrt::TraceVariant v = variant_for(t, flags);
     int perCU = 0;
-    const mrt_launch_cfg cfg = effective_cfg(t, numRays);
+    mrt_launch_cfg cfg = effective_cfg(t, numRays);
+    // autotuning: the schedule candidate this launch uses, and its timing slot
+    TuneState* tune = nullptr;
+    TuneState::Pending* slot = nullptr;
+    int cand = -1;
+    const mrt_launch_cfg& uc = t->cfg;
+    if (uc.autotune && uc.num_queues < 0 && uc.waves_per_cu == 0 && uc.fetch_threshold == 0 && uc.lane_groups == 1 &&
+        !(flags & MRT_TRACE_STATS)) {
+        const auto key = std::make_pair(numRays, variant_key(v));
+        auto it = t->tunes.find(key);
+        if (it != t->tunes.end()) {
+            tune = it->second;
+        } else if ((int)t->tunes.size() < kMaxTuned) {
+            tune = new TuneState();
+            tune->stream = stream;
+            t->tunes[key] = tune;
+        }
+        // A batch size launched on several streams keeps the fixed rule: its launches
+        // overlap, and a schedule's time alone no longer ranks the pipeline (the
+        // bench's two-stream hairball buffer: 5.2 ms on the rule, 6.2 tuned alone).
+        if (tune && tune->stream != stream) tune->multiStream = true;
+        if (tune && tune->multiStream) tune = nullptr;
+    }
+    if (tune) {
+        tune_collect(tune);
+        if (tune->locked >= 0) {
+            cand = tune->locked;
+        } else {
+            cand = tune->next;
+            tune->next = (tune->next + 1) % TuneState::kCandidates;
+            for (auto& p : tune->pending)
+                if (p.cand < 0) {
+                    slot = &p;
+                    break;
+                }
+            if (slot && !slot->start) {
+                MRT_HIP(hipEventCreate(&slot->start));
+                MRT_HIP(hipEventCreate(&slot->stop));
+            }
+        }
+        cfg = tune_candidate(cfg, cand);
+    }
     const int blocks = grid_blocks(t, cfg, v, numRays, &perCU);
     const int totalLanes = blocks * mrt::kBlockThreads;
     mrt::Workspace* ws = nullptr;
@@ -350,8 +476,15 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     // one leaves the counter sticky (mrt_tracer_stack_overflows reads it).
     if (info) MRT_HIP(hipMemsetAsync(ws->status, 0, sizeof(int), s));
     if (info) MRT_HIP(hipEventRecord(t->evStart, s));
+    if (slot) MRT_HIP(hipEventRecord(slot->start, s));
     MRT_HIP(mrt::launch_trace(v, a, blocks, s));
+    if (slot) {
+        MRT_HIP(hipEventRecord(slot->stop, s));
+        slot->cand = cand;
+    }
     if (info) {
+        info->autotune_candidate = cand;
+        info->autotune_locked = tune && tune->locked >= 0 ? 1 : 0;
         MRT_HIP(hipEventRecord(t->evStop, s));
         MRT_HIP(hipEventSynchronize(t->evStop));
         MRT_HIP(hipEventElapsedTime(&info->kernel_ms, t->evStart, t->evStop));
@@ -475,6 +608,7 @@ int mrt_tracer_destroy(mrt_tracer* t) {
         }
         if (t->evStart) (void)hipEventDestroy(t->evStart);
         if (t->evStop) (void)hipEventDestroy(t->evStop);
+        tune_reset(t);
     }
     delete t;
     return MRT_OK;
@@ -498,6 +632,8 @@ int mrt_tracer_bind(mrt_tracer* t, const void* nodes, int64_t nodeBytes, const v
     t->triIndexBytes = triIndexBytes;
     t->bound = true;
     t->wideBuiltFor = -1;   // a new BVH: its wide nodes are derived now (if configured)
+    DeviceGuard guard(t->device);
+    tune_reset(t);          // and its schedules are tuned again
     return refresh_wide(t);
 }
 
@@ -521,9 +657,12 @@ int mrt_tracer_set_config(mrt_tracer* t, const mrt_launch_cfg* cfg) {
     if (c.wide < 0) c.wide = d.wide;   // -1 = library default
     if (c.spec_slack < 0) c.spec_slack = d.spec_slack;
     if (c.static_rounds == 0) c.static_rounds = d.static_rounds;
+    if (c.autotune < 0) c.autotune = d.autotune;
     if (!valid_cfg(c)) return fail(MRT_ERR_INVALID_ARG, "launch config out of range");
     std::lock_guard<std::mutex> lock(t->mu);
     t->cfg = c;
+    DeviceGuard guard(t->device);
+    tune_reset(t);
     return refresh_wide(t);
 }
 

@@ -123,14 +123,40 @@ def test_automatic_launch_config(env, name, queues, waves):
     e = scenes.get(bench.workload_spec(name)[0])
     batches = bench.Batches(name, e["scene"], e["gbvh"], tracer)
     rb = batches.batches[0][0]
+    saved = tracer.config()
+    tracer.set_config(autotune=0)   # the fixed rule (autotuning starts from it and may pick another schedule)
     tracer.trace_batch(rb, exact_rcp=True)
+    tracer.set_config(**saved)
     assert tracer.last_info["num_queues"] == queues
     assert tracer.last_info["fetch_threshold"] == (48 if queues else 0)
     assert tracer.last_info["grid_waves"] == waves * torch.cuda.get_device_properties(0).multi_processor_count
     saved = tracer.config()
     try:
-        tracer.set_config(waves_per_cu=20)   # any explicit distribution knob keeps the static rounds
+        tracer.set_config(waves_per_cu=20, autotune=0)   # any explicit distribution knob keeps the static rounds
         tracer.trace_batch(rb, exact_rcp=True)
         assert tracer.last_info["num_queues"] == 0
     finally:
         tracer.set_config(**saved)
+
+
+def test_autotuned_schedule_settles_and_keeps_results(env):
+    """cfg.autotune (default): the first launches of a batch size cycle through five
+    ray-distribution schedules, timed without blocking, then keep the fastest. Every
+    launch, exploring or settled, returns the oracle's closest hits."""
+    bench, scenes, tracer, threads = env
+    name = "bunny-primary-1024x768"
+    e = scenes.get(bench.workload_spec(name)[0])
+    bufs = scenes.host_buffers(bench.workload_spec(name)[0])
+    batches = bench.Batches(name, e["scene"], e["gbvh"], tracer)
+    rb = batches.batches[0][0]
+    assert tracer.config()["autotune"] == 1
+    tracer.set_config(autotune=1)   # a fresh tuning state for this handle
+    want, _, _ = O.trace(rb.rays.cpu().numpy(), *bufs, threads=threads)
+    seen = set()
+    for i in range(40):
+        tracer.trace_batch(rb, exact_rcp=True)   # blocking: every launch's timing is read back by the next
+        seen.add(tracer.last_info["autotune_candidate"])
+        got = rb.results_numpy()
+        assert np.array_equal(got[:, :2], want[:, :2]), f"launch {i} (candidate {tracer.last_info['autotune_candidate']})"
+    assert seen == {0, 1, 2, 3, 4} or tracer.last_info["autotune_locked"] == 1
+    assert tracer.last_info["autotune_locked"] == 1

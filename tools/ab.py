@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--workload", action="append", help="repeatable")
     ap.add_argument("--variant", action="append", required=True, help="libdir:json-config")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--warm-rounds", type=int, default=1, help="untimed rounds first (autotuning settles there)")
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--fast-rcp", action="store_true")
     args = ap.parse_args()
@@ -85,7 +86,7 @@ def run(args, workload):
         variants.append((spec, lib, h))
     ref = None
     times = {spec: [] for spec, _, _ in variants}
-    for r in range(args.rounds + 1):
+    for r in range(args.rounds + args.warm_rounds):
         for spec, lib, h in variants:
             launches = []
             for rb, _ in b.batches:
@@ -99,7 +100,7 @@ def run(args, workload):
                     lib.mrt_tracer_trace(h, rp, res, n, fl, None, stream.cuda_stream)
             e1.record(stream)
             torch.cuda.synchronize()
-            if r > 0:
+            if r >= args.warm_rounds:
                 times[spec].append(e0.elapsed_time(e1) / (args.launches * len(launches)))
             out = b.batches[-1][0].results_numpy()[:, :2].copy()
             if ref is None:

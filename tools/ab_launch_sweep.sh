@@ -13,4 +13,4 @@ fi
 ARGS=()
 for w in $W; do ARGS+=(--workload "$w"); done
 for c in "${CFGS[@]}"; do case "$c" in "{"*) ARGS+=(--variant "lib:$c") ;; *) ARGS+=(--variant "$c") ;; esac; done
-timeout -k 10 700 python tools/ab.py "${ARGS[@]}" 2>&1 | grep -v amdgpu.ids
+timeout -k 10 700 python tools/ab.py --warm-rounds ${WARM_ROUNDS:-1} "${ARGS[@]}" 2>&1 | grep -v amdgpu.ids
