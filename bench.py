@@ -456,6 +456,11 @@ def roofline(name, alg_bytes_per_launch, kernel_ms, bvh_bytes):
     return out
 
 
+# cfg.autotune candidates (csrc/mrt_api.cpp tune_candidate)
+SCHEDULES = {0: "static rounds, 20 waves/CU", 1: "static rounds, 8 waves/CU", 2: "8 per-XCD queues",
+             3: "global queue, refill at 48, 16 waves/CU", 4: "global queue, refill at 48, 12 waves/CU"}
+
+
 def run_workload(name, tracer, scenes, world, rank, steps, warmup, exact, want_cpu):
     scene_name = workload_spec(name)[0]
     e = scenes.get(scene_name)
@@ -470,6 +475,13 @@ def run_workload(name, tracer, scenes, world, rank, steps, warmup, exact, want_c
     alg_bytes = reduce_over_ranks(alg_bytes, world, "sum") / world   # per-GPU bytes (mean over ranks)
     value = counted * steps / wall / 1e6
     gather = gather_to_root(batches, world) if world > 1 else None
+    # the schedule the launches ran on (cfg.autotune settles during the warmup):
+    # one more blocking launch of the first batch, outside the timed region
+    tracer.trace_batch(batches.batches[0][0], exact_rcp=exact)
+    li = tracer.last_info
+    schedule = {"autotune_candidate": li["autotune_candidate"], "autotune_locked": li["autotune_locked"],
+                "name": SCHEDULES.get(li["autotune_candidate"], "fixed rule"), "num_queues": li["num_queues"],
+                "fetch_threshold": li["fetch_threshold"], "grid_waves": li["grid_waves"]}
     g = e["gbvh"]
     out = {
         "workload": name,
@@ -492,6 +504,7 @@ def run_workload(name, tracer, scenes, world, rank, steps, warmup, exact, want_c
         "per_ray": {"nodes": round(n_nodes / batches.rays_traced, 2), "tris": round(n_tris / batches.rays_traced, 2),
                     "leaves": round(n_leaves / batches.rays_traced, 2),
                     "bytes": round(alg_bytes / batches.rays_traced, 1)},
+        "schedule": schedule,
         "roofline": roofline(name, alg_bytes / len(batches.batches), launch_ms, g.total_bytes),
         "reference_mrays": REFERENCE_MRAYS.get(name),
     }
