@@ -54,9 +54,9 @@ struct mrt_tracer {
     std::vector<mrt::Workspace*> workspaces;
     hipEvent_t evStart = nullptr, evStop = nullptr;
 
-    // Occupancy per kernel variant, queried once (hipOccupancy* is a host
-    // round-trip that would otherwise sit on every launch).
-    int occ[128] = {};
+    // Occupancy per kernel variant (index variant_key(), below 256), queried once
+    // (hipOccupancy* is a host round-trip that would otherwise sit on every launch).
+    int occ[256] = {};
 
     // cfg.autotune: per (batch size, variant) the ray-distribution schedule the
     // measured launches chose (mrt_api.cpp autotune_*), reset on bind/set_config.
@@ -198,8 +198,10 @@ constexpr int kAutoMinWaves = 8;
 // workgroup is resident at once.
 int variant_key(const mrt::TraceVariant& v) {
     const int lds = v.ldsStack == 8 ? 0 : v.ldsStack == 16 ? 1 : 2;
+    static_assert((15 | (2 << 4) | (mrt::kNodeWide4Q << 6)) < (int)(sizeof(mrt_tracer::occ) / sizeof(int)),
+                  "every variant_key indexes mrt_tracer::occ");
     return (v.anyHit ? 1 : 0) | (v.speculative ? 2 : 0) | (v.exactRcp ? 4 : 0) | (v.stats ? 8 : 0) | (lds << 4) |
-           (v.nodes << 6);
+           (v.nodes << 6);   // < 256 = the size of mrt_tracer::occ
 }
 
 // The launch configuration a trace uses: the tracer's, except that with every
