@@ -65,7 +65,7 @@ struct mrt_tracer {
 
 // Launch-schedule autotuning state of one (batch size, kernel variant).
 struct TuneState {
-    static constexpr int kCandidates = 5;
+    static constexpr int kCandidates = 7;
     static constexpr int kSamples = 3;   // timed launches per candidate (the minimum counts)
     float best[kCandidates];
     int samples[kCandidates] = {};
@@ -328,7 +328,7 @@ int refresh_wide(mrt_tracer* t) {
 // cache residency (profiles/round2_tuning.md: static rounds, fewer waves, per-XCD
 // queues and the global queue each win somewhere by 5-70 %). With cfg.autotune
 // and the distribution knobs at their defaults, the first launches of a batch
-// size cycle through these candidates, each timed with an event pair that is
+// size cycle through these seven candidates, each timed with an event pair that is
 // read back on a later launch (never blocking), and after kSamples launches each
 // the fastest is kept for that batch size. Results do not depend on the schedule
 // (closest hits are the same hits; an any-hit ray may report a different valid hit).
@@ -341,10 +341,12 @@ mrt_launch_cfg tune_candidate(const mrt_launch_cfg& base, int c) {
     x.num_queues = -1;
     switch (c) {
         case 0: break;                                                      // static rounds, 20 waves/CU
-        case 1: x.waves_per_cu = 8; break;                                  // static rounds, 8 waves/CU
+        case 1: x.waves_per_cu = 8; break;                                  // static rounds, fewer waves
         case 2: x.num_queues = 8; break;                                    // per-XCD queues
         case 3: x.num_queues = 1; x.fetch_threshold = 48; x.waves_per_cu = 16; break;   // global queue
-        default: x.num_queues = 1; x.fetch_threshold = 48; x.waves_per_cu = 12; break;
+        case 4: x.num_queues = 1; x.fetch_threshold = 48; x.waves_per_cu = 12; break;
+        case 5: x.waves_per_cu = 16; break;
+        default: x.waves_per_cu = 12; break;
     }
     return x;
 }
