@@ -685,10 +685,10 @@ def main():
             "strong_scaling": strong,
             "detail": {k: head[k] for k in ("kernel_ms_per_launch", "rays_traced", "mrays_traced_per_s", "bvh",
                                             "per_ray", "reference_mrays", "rays_counted_all_ranks", "gather",
-                                            "warmup_steps_run")},
+                                            "warmup_steps_run", "schedule")},
             "extra_workloads": [{k: r.get(k) for k in ("workload", "value", "reference_mrays", "kernel_ms_per_launch",
                                                        "rays_counted", "rays_traced", "per_ray", "roofline", "bvh",
-                                                       "cpu_baseline")}
+                                                       "cpu_baseline", "schedule")}
                                 for r in extras],
         }
         print(json.dumps(line), flush=True)

@@ -66,7 +66,9 @@ struct mrt_tracer {
 // Launch-schedule autotuning state of one (batch size, kernel variant).
 struct TuneState {
     static constexpr int kCandidates = 7;
-    static constexpr int kSamples = 3;   // timed launches per candidate (the minimum counts)
+    static constexpr int kSamples = 4;   // timed launches per candidate (the minimum counts)
+    int launches = 0;    // exploring launches so far (the first round of candidates runs untimed:
+                         // the clocks and caches are still settling)
     float best[kCandidates];
     int samples[kCandidates] = {};
     int next = 0;        // candidate the next exploring launch uses
@@ -434,11 +436,12 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
         } else {
             cand = tune->next;
             tune->next = (tune->next + 1) % TuneState::kCandidates;
-            for (auto& p : tune->pending)
-                if (p.cand < 0) {
-                    slot = &p;
-                    break;
-                }
+            if (tune->launches++ >= TuneState::kCandidates)
+                for (auto& p : tune->pending)
+                    if (p.cand < 0) {
+                        slot = &p;
+                        break;
+                    }
             if (slot && !slot->start) {
                 MRT_HIP(hipEventCreate(&slot->start));
                 MRT_HIP(hipEventCreate(&slot->stop));

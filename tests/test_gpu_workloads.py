@@ -153,7 +153,7 @@ def test_autotuned_schedule_settles_and_keeps_results(env):
     tracer.set_config(autotune=1)   # a fresh tuning state for this handle
     want, _, _ = O.trace(rb.rays.cpu().numpy(), *bufs, threads=threads)
     seen = set()
-    for i in range(50):
+    for i in range(60):
         tracer.trace_batch(rb, exact_rcp=True)   # blocking: every launch's timing is read back by the next
         seen.add(tracer.last_info["autotune_candidate"])
         got = rb.results_numpy()
