@@ -95,9 +95,8 @@ typedef struct mrt_launch_cfg {
     int32_t autotune;          /* 1 = with the distribution knobs above at their defaults, the first launches
                                   of each batch size (per kernel variant, up to 64 sizes) time seven ray-
                                   distribution schedules (static rounds at 20, 16, 12 or 8 waves/CU, per-XCD
-                                  queues, the global queue at 16 or 12 waves/CU) three times each without
-                                  blocking (after one untimed round of them) and
-                                  keep the fastest (a batch size launched on more than one stream keeps the
+                                  queues, the global queue at 16 or 12 waves/CU) four times each without
+                                  blocking, after one untimed round of them, and keep the fastest (a batch size launched on more than one stream keeps the
                                   fixed rule); reset by bind and set_config (default 1). 0 = the fixed
                                   rule only; -1 = library default */
 } mrt_launch_cfg;
