@@ -46,6 +46,7 @@ struct mrt_tracer {
     int64_t wideBytes = 0;
     int wideBuiltFor = -1;   // the cfg.wide value the current array was built for
     int wideFormat = mrt::kNodeCompact2;   // the form wideNodes holds (kNodeWide4 / kNodeWide4Q)
+    bool wideLeafCounts = false;           // its leaf refs carry triangle counts
 
     // Launch scratch, one set per stream the handle has launched on: the stack
     // spill slab, the queue heads and the overflow counter are written by a
@@ -308,11 +309,21 @@ int refresh_wide(mrt_tracer* t) {
     if (want) {
         std::vector<int32_t> host((size_t)(t->nodeBytes / 4));
         MRT_HIP(hipMemcpy(host.data(), t->nodes, (size_t)t->nodeBytes, hipMemcpyDeviceToHost));
+        // The first word of every Woop slot (the terminators): the leaf refs carry counts.
+        const int64_t slots = t->woopBytes / 16;
+        const bool counts = mrt::leaf_counts_fit(slots);
+        std::vector<int32_t> woopX;
+        if (counts) {
+            woopX.resize((size_t)slots);
+            MRT_HIP(hipMemcpy2D(woopX.data(), 4, t->woop, 16, 4, (size_t)slots, hipMemcpyDeviceToHost));
+        }
+        const int32_t* wx = counts ? woopX.data() : nullptr;
         std::vector<uint32_t> wide;
         int format = mrt::kNodeWide4;
         // The quantized form when asked for and every box quantizes; else the exact one.
-        if (want == 2 && mrt::build_wide4q(host.data(), t->nodeBytes / 64, &wide)) format = mrt::kNodeWide4Q;
-        else wide = mrt::build_wide4(host.data(), t->nodeBytes / 64);
+        if (want == 2 && mrt::build_wide4q(host.data(), t->nodeBytes / 64, &wide, wx, slots)) format = mrt::kNodeWide4Q;
+        else wide = mrt::build_wide4(host.data(), t->nodeBytes / 64, wx, slots);
+        t->wideLeafCounts = counts;
         const int64_t bytes = (int64_t)wide.size() * 4;
         if (bytes > mrt::kMaxBufferBytes) return fail(MRT_ERR_TOO_LARGE, "4-wide node array above the 32-bit range");
         MRT_HIP(hipMalloc(&t->wideNodes, (size_t)bytes));
@@ -468,6 +479,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     a.fetchThreshold = cfg.fetch_threshold;
     a.specSlack = cfg.spec_slack;
     a.staticRounds = cfg.static_rounds;
+    a.wideLeafCounts = wide && t->wideLeafCounts;
     a.laneGroupsLog2 = __builtin_ctz((unsigned)cfg.lane_groups);
     a.totalLanes = totalLanes;
     a.queues = ws->queues;
@@ -706,16 +718,26 @@ int mrt_tracer_stack_overflows(mrt_tracer* t, int64_t* count, int32_t reset) {
     return MRT_OK;
 }
 
-int mrt_derive_wide_nodes(const void* nodes, int64_t nodeBytes, int32_t form, void* out, int64_t outCapacity,
-                          int64_t* outBytes) {
-    if (!nodes || !outBytes || nodeBytes <= 0 || nodeBytes % 64 != 0 || (form != 1 && form != 2))
+int mrt_derive_wide_nodes(const void* nodes, int64_t nodeBytes, const void* woop, int64_t woopBytes, int32_t form,
+                          void* out, int64_t outCapacity, int64_t* outBytes) {
+    if (!nodes || !outBytes || nodeBytes <= 0 || nodeBytes % 64 != 0 || (form != 1 && form != 2) ||
+        (woop && (woopBytes <= 0 || woopBytes % 16 != 0)))
         return fail(MRT_ERR_INVALID_ARG, "derive_wide_nodes: bad arguments");
+    // the first word of every Woop slot, when the leaf refs can carry counts
+    const int64_t slots = woop ? woopBytes / 16 : 0;
+    std::vector<int32_t> woopX;
+    if (woop && mrt::leaf_counts_fit(slots)) {
+        woopX.resize((size_t)slots);
+        for (int64_t i = 0; i < slots; i++) woopX[(size_t)i] = static_cast<const int32_t*>(woop)[4 * i];
+    }
+    const int32_t* wx = woopX.empty() ? nullptr : woopX.data();
     std::vector<uint32_t> wide;
     const auto* n = static_cast<const int32_t*>(nodes);
     if (form == 2) {
-        if (!mrt::build_wide4q(n, nodeBytes / 64, &wide)) return fail(MRT_ERR_INVALID_ARG, "a box has no finite quantization");
+        if (!mrt::build_wide4q(n, nodeBytes / 64, &wide, wx, slots))
+            return fail(MRT_ERR_INVALID_ARG, "a box has no finite quantization");
     } else {
-        wide = mrt::build_wide4(n, nodeBytes / 64);
+        wide = mrt::build_wide4(n, nodeBytes / 64, wx, slots);
     }
     *outBytes = (int64_t)wide.size() * 4;
     if (out) {

@@ -39,6 +39,7 @@ struct TraceArgs {
     int fetchThreshold;        // refill when fewer live lanes than this
     int specSlack;             // speculative: leave the node loop once <= this many lanes lack a leaf
     int staticRounds;          // queue modes: static strided rounds of the grid before the queues
+    int wideLeafCounts;        // the wide leaf refs carry triangle counts (wide_bvh.cpp)
     int laneGroupsLog2;        // strided mode: a wave's lanes take rays from 2^k spread-out sub-ranges
     int totalLanes;            // grid lanes (stride of the spill slab)
     unsigned* queues;          // numQueues heads, kQueueStrideWords apart, zeroed per launch
@@ -63,10 +64,17 @@ struct TraceVariant {
 
 // The 4-wide node array derived from a Compact2 node array (numNodes inner nodes,
 // 16 int32 each): 32 uint32 (128 B) per wide node, layout in wide_bvh.cpp.
-std::vector<uint32_t> build_wide4(const int32_t* nodes, int64_t numNodes);
+// woopX (the first word of each of woopSlots Woop slots, or null): with it the
+// leaf refs carry their triangle counts (wide_bvh.cpp); pass it only when
+// leaf_counts_fit(woopSlots) (woop indices below 2^27).
+constexpr int kWideLeafAddrBits = 27;
+bool leaf_counts_fit(int64_t woopSlots);
+std::vector<uint32_t> build_wide4(const int32_t* nodes, int64_t numNodes, const int32_t* woopX = nullptr,
+                                  int64_t woopSlots = 0);
 // The quantized 4-wide form: 16 uint32 (64 B) per wide node. False (and no
 // output) when some child box has no finite quantization (non-finite planes).
-bool build_wide4q(const int32_t* nodes, int64_t numNodes, std::vector<uint32_t>* out);
+bool build_wide4q(const int32_t* nodes, int64_t numNodes, std::vector<uint32_t>* out, const int32_t* woopX = nullptr,
+                  int64_t woopSlots = 0);
 
 // Launch one persistent trace. grid = number of 256-thread workgroups.
 hipError_t launch_trace(const TraceVariant& v, const TraceArgs& a, int gridBlocks, hipStream_t s);

@@ -15,7 +15,11 @@
 //             leaf = the Compact2 leaf ref (~woop float4 index), absent = 0x76543210
 //             (an absent child's planes are NaN: its slab test always fails)
 //   float4 7  unused (zero)
-// Leaves, Woop triangles and triIndex are the Compact2 ones: the leaf loop is unchanged.
+// Leaves, Woop triangles and triIndex are the Compact2 ones. Given the first word of
+// every Woop slot (leaf_counts_fit), a leaf ref carries its triangle count:
+// ~(woop index | count << 27) with count 1..15 (0 = not counted: the leaf ends at
+// its terminator, as in the binary step), so the leaf loop neither loads the
+// terminator nor a triangle slot past it.
 //
 // The quantized form (build_wide4q) stores the same four children in 64 B, four
 // 16-B loads instead of seven (the traversal is bound by 16-B lane loads,
@@ -32,6 +36,7 @@
 // box therefore contains the binary box, its slab interval contains the binary
 // one (the slab values are monotonic in the plane), and the traversal tests a
 // superset of the leaves the binary traversal tests.
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
@@ -90,6 +95,22 @@ int collapse(const int32_t* nodes, int32_t ref, Child out[4]) {
         n++;
     }
     return n;
+}
+
+// The ref a wide child stores for Compact2 leaf ref `ref` (see above).
+int32_t wide_leaf_ref(int32_t ref, const int32_t* woopX, int64_t woopSlots) {
+    if (!woopX) return ref;
+    const int64_t slot = ~(int64_t)ref;
+    int32_t count = 0;
+    for (int32_t k = 0; k <= 15; k++) {
+        const int64_t s = slot + 3 * (int64_t)k;
+        if (s >= woopSlots) break;
+        if (woopX[s] == (int32_t)0x80000000) {
+            count = k;
+            break;
+        }
+    }
+    return ~(int32_t)(slot | ((int64_t)count << kWideLeafAddrBits));
 }
 
 // f32 with denormals flushed to (signed) zero, as the kernel computes.
@@ -152,7 +173,10 @@ void number_wide(const int32_t* nodes, int64_t numNodes, std::vector<int32_t>& w
 
 }  // namespace
 
-bool build_wide4q(const int32_t* nodes, int64_t numNodes, std::vector<uint32_t>* out) {
+bool leaf_counts_fit(int64_t woopSlots) { return woopSlots <= ((int64_t)1 << kWideLeafAddrBits); }
+
+bool build_wide4q(const int32_t* nodes, int64_t numNodes, std::vector<uint32_t>* out, const int32_t* woopX,
+                  int64_t woopSlots) {
     out->clear();
     if (numNodes <= 0) return true;
     std::vector<int32_t> wideOf, order;
@@ -185,14 +209,14 @@ bool build_wide4q(const int32_t* nodes, int64_t numNodes, std::vector<uint32_t>*
         o[3] = exps;
         for (int c = 0; c < 4; c++) {
             int32_t ref = kEntrypointSentinel;
-            if (c < n) ref = ch[c].ref >= 0 ? wideOf[(size_t)(ch[c].ref / 4)] * 4 : ch[c].ref;
+            if (c < n) ref = ch[c].ref >= 0 ? wideOf[(size_t)(ch[c].ref / 4)] * 4 : wide_leaf_ref(ch[c].ref, woopX, woopSlots);
             o[12 + c] = (uint32_t)ref;
         }
     }
     return true;
 }
 
-std::vector<uint32_t> build_wide4(const int32_t* nodes, int64_t numNodes) {
+std::vector<uint32_t> build_wide4(const int32_t* nodes, int64_t numNodes, const int32_t* woopX, int64_t woopSlots) {
     std::vector<uint32_t> out;
     if (numNodes <= 0) return out;
     // Pass 1: number the wide nodes depth first (binary node -> wide index).
@@ -215,7 +239,7 @@ std::vector<uint32_t> build_wide4(const int32_t* nodes, int64_t numNodes) {
                     lo[k] = ch[c].lo[k];
                     hi[k] = ch[c].hi[k];
                 }
-                ref = ch[c].ref >= 0 ? wideOf[(size_t)(ch[c].ref / 4)] * 8 : ch[c].ref;
+                ref = ch[c].ref >= 0 ? wideOf[(size_t)(ch[c].ref / 4)] * 8 : wide_leaf_ref(ch[c].ref, woopX, woopSlots);
             }
             for (int k = 0; k < 3; k++) {
                 std::memcpy(&o[(2 * k + f4) * 4 + pair], &lo[k], 4);

@@ -68,7 +68,7 @@ TRACE_SYMBOLS = [
     ("mrt_tracer_trace", i32, [vp, vp, vp, i32, u32, vp, vp]),
     ("mrt_tracer_trace_timed", i32, [vp, vp, vp, i32, u32, vp, vp, C.POINTER(TraceInfo)]),
     ("mrt_tracer_stack_overflows", i32, [vp, C.POINTER(i64), i32]),
-    ("mrt_derive_wide_nodes", i32, [vp, i64, i32, vp, i64, C.POINTER(i64)]),
+    ("mrt_derive_wide_nodes", i32, [vp, i64, vp, i64, i32, vp, i64, C.POINTER(i64)]),
     ("mrt_bind_bvh", i32, [vp, i64, vp, i64, vp, i64]),
     ("mrt_unbind_bvh", i32, []),
     ("mrt_trace", i32, [vp, vp, i32, i32, vp, C.POINTER(f32)]),

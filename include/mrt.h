@@ -155,11 +155,13 @@ int  mrt_tracer_stack_overflows(mrt_tracer* t, int64_t* count, int32_t reset);
 /* Host-only (no device): the 4-wide node array a tracer derives at bind time
  * from a Compact2 node array (host memory). form 1 = exact child boxes, 128 B per
  * node; form 2 = child boxes quantized outward, 64 B per node (layouts in
- * csrc/wide_bvh.cpp). *outBytes = the array's size; it is copied to out when
+ * csrc/wide_bvh.cpp). With the Woop array (host memory, may be NULL) the leaf refs
+ * carry their triangle counts, as the tracer's own array does when the woop
+ * indices fit 27 bits. *outBytes = the array's size; it is copied to out when
  * out != NULL and outCapacity suffices (else MRT_ERR_TOO_LARGE). Form 2 returns
  * MRT_ERR_INVALID_ARG when some box has no finite quantization. */
-int  mrt_derive_wide_nodes(const void* nodes, int64_t nodeBytes, int32_t form, void* out, int64_t outCapacity,
-                           int64_t* outBytes);
+int  mrt_derive_wide_nodes(const void* nodes, int64_t nodeBytes, const void* woop, int64_t woopBytes, int32_t form,
+                           void* out, int64_t outCapacity, int64_t* outBytes);
 
 /* Diagnostics: run the EXACT variants' reciprocal (v_rcp_f32 + one FMA Newton step)
  * against the correctly rounded 1.0f / x for all 2^32 inputs on the current device;

@@ -25,14 +25,16 @@ SENTINEL = 0x76543210
 FLT_MIN = np.float32(1.17549435e-38)
 
 
-def derive(nodes, form):
+def derive(nodes, form, woop=None):
     lib = _lib.trace_lib()
     nodes = np.ascontiguousarray(nodes)
+    wp, wb = (None, 0) if woop is None else (np.ascontiguousarray(woop).ctypes.data, woop.nbytes)
     size = C.c_int64(0)
-    rc = lib.mrt_derive_wide_nodes(nodes.ctypes.data, nodes.nbytes, form, None, 0, C.byref(size))
+    rc = lib.mrt_derive_wide_nodes(nodes.ctypes.data, nodes.nbytes, wp, wb, form, None, 0, C.byref(size))
     assert rc == 0, _lib.trace_lib().mrt_last_error_detail()
     out = np.zeros(size.value // 4, np.uint32)
-    rc = lib.mrt_derive_wide_nodes(nodes.ctypes.data, nodes.nbytes, form, out.ctypes.data, out.nbytes, C.byref(size))
+    rc = lib.mrt_derive_wide_nodes(nodes.ctypes.data, nodes.nbytes, wp, wb, form, out.ctypes.data, out.nbytes,
+                                   C.byref(size))
     assert rc == 0
     return out
 
@@ -80,11 +82,12 @@ def trees(request):
     scene = mrt.Scene.synthetic(request.param, 0, 1)
     nodes, woop, tri = mrt.Bvh.build(scene).buffers()
     nodes = np.ascontiguousarray(nodes).view(np.int32).reshape(-1)
-    return nodes, derive(nodes, 1), derive(nodes, 2)
+    woop = np.ascontiguousarray(woop).view(np.int32).reshape(-1)
+    return nodes, derive(nodes, 1), derive(nodes, 2), woop
 
 
 def test_both_forms_have_the_same_children(trees):
-    nodes, w, q = trees
+    nodes, w, q, _ = trees
     assert w.size // 32 == q.size // 16
     rw = w.reshape(-1, 32)[:, 24:28].view(np.int32)
     rq = q.reshape(-1, 16)[:, 12:16].view(np.int32)
@@ -102,7 +105,7 @@ def test_both_forms_have_the_same_children(trees):
 
 
 def test_exact_form_keeps_the_compact2_boxes(trees):
-    nodes, w, _ = trees
+    nodes, w, _, _ = trees
     lo, hi = exact_boxes(w)
     refs = w.reshape(-1, 32)[:, 24:28].view(np.int32)
     present = refs != SENTINEL
@@ -117,7 +120,7 @@ def test_exact_form_keeps_the_compact2_boxes(trees):
 
 
 def test_quantized_boxes_contain_the_exact_boxes(trees):
-    _, w, q = trees
+    _, w, q, _ = trees
     elo, ehi = exact_boxes(w)
     qlo, qhi = decode_quantized(q)
     refs = w.reshape(-1, 32)[:, 24:28].view(np.int32)
@@ -165,5 +168,33 @@ def test_non_finite_boxes_are_refused_by_the_quantized_form():
     n[12], n[13] = ~0, ~3
     lib = _lib.trace_lib()
     size = C.c_int64(0)
-    assert lib.mrt_derive_wide_nodes(n.ctypes.data, n.nbytes, 2, None, 0, C.byref(size)) == _lib.MRT_ERR_INVALID_ARG
-    assert lib.mrt_derive_wide_nodes(n.ctypes.data, n.nbytes, 1, None, 0, C.byref(size)) == 0
+    assert lib.mrt_derive_wide_nodes(n.ctypes.data, n.nbytes, None, 0, 2, None, 0, C.byref(size)) == _lib.MRT_ERR_INVALID_ARG
+    assert lib.mrt_derive_wide_nodes(n.ctypes.data, n.nbytes, None, 0, 1, None, 0, C.byref(size)) == 0
+
+
+def test_leaf_refs_carry_their_triangle_counts(trees):
+    """With the Woop array the leaf refs are ~(woop index | count << 27): the index is the
+    Compact2 leaf ref's, the count the triangles before the leaf's terminator (1..15;
+    0 = longer, found by the terminator). Inner refs and boxes are unchanged."""
+    nodes, w, q, woop = trees
+    for form, plain in ((1, w), (2, q)):
+        counted = derive(nodes, form, woop)
+        stride = 32 if form == 1 else 16
+        refs_off = 24 if form == 1 else 12
+        rp = plain.reshape(-1, stride)[:, refs_off:refs_off + 4].view(np.int32)
+        rc = counted.reshape(-1, stride)[:, refs_off:refs_off + 4].view(np.int32)
+        leaf = rp < 0
+        assert np.array_equal(rc[~leaf], rp[~leaf])
+        other = np.ones(stride, bool)
+        other[refs_off:refs_off + 4] = False
+        assert np.array_equal(counted.reshape(-1, stride)[:, other], plain.reshape(-1, stride)[:, other])
+        lr = (~rc[leaf]).astype(np.int64)
+        slot, count = lr & ((1 << 27) - 1), lr >> 27
+        assert np.array_equal(slot, (~rp[leaf]).astype(np.int64))
+        wx = woop.reshape(-1, 4)[:, 0]
+        term = np.int32(-2147483648)
+        for s0, c in zip(slot[:5000], count[:5000]):
+            if c == 0:
+                assert all(wx[s0 + 3 * k] != term for k in range(16) if s0 + 3 * k < len(wx))
+            else:
+                assert wx[s0 + 3 * c] == term and all(wx[s0 + 3 * k] != term for k in range(c))
