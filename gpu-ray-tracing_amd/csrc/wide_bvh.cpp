@@ -12,7 +12,7 @@
 //   float4 2  the same for y                           float4 3
 //   float4 4  the same for z                           float4 5
 //   float4 6  child refs (int): inner = float4 index of the wide node (8 per node),
-//             leaf = the Compact2 leaf ref (~woop float4 index), absent = 0x76543210
+//             leaf = ~(woop float4 index [| count << 27, below]), absent = 0x76543210
 //             (an absent child's planes are NaN: its slab test always fails)
 //   float4 7  unused (zero)
 // Leaves, Woop triangles and triIndex are the Compact2 ones. Given the first word of
@@ -29,7 +29,7 @@
 //   float4 1  (qlo.x, qhi.x, qlo.y, qhi.y)  one byte per child (child c = byte c)
 //   float4 2  (qlo.z, qhi.z, 0, 0)
 //   float4 3  child refs: inner = float4 index of the wide node (4 per node),
-//             leaf = the Compact2 leaf ref, absent = 0x76543210
+//             leaf = as in the exact form, absent = 0x76543210
 // A child plane decodes as fma(q, 2^e, origin) in f32 with denormals flushed —
 // the kernel's arithmetic exactly — and q is chosen so that the decoded lower
 // plane is <= the Compact2 plane and the decoded upper plane >= it. The decoded
