@@ -91,8 +91,10 @@ HEADLINE = "bunny-primary-1024x768"
 EXTRA_N1 = ["bunny-primary-640x480", "conference-ao-640x480", "sponza-diffuse-640x480", "sponza-diffuse2-640x480",
             "hairball-diffuse-640x480", "hairball-diffuse-1920x1080"]
 # Strong-scaling config: scene, frame, samples per pixel, rays per launch.
+# min_launches: a shard is cut into at least this many launches (alternating over two streams).
 STRONG = {"name": "hairball-diffuse-1920x1080x8spp", "scene": "hairball", "w": 1920, "h": 1080, "spp": 8,
-          "max_batch": 1 << 21}
+          "max_batch": 1 << 21, "min_launches": 1, "block": 1 << 14, "streams": 2}
+STRONG_PROJECT = (2, 4, 8)   # N=1 only: rank counts whose per-rank shards are timed on the one GPU
 
 
 def workload_spec(name):
@@ -329,15 +331,46 @@ def algorithmic_bytes(tracer, batches):
     return total, nodes, tris, leaves
 
 
+def joined(launches):
+    """The launches of one step, as one callable. When they span several streams the
+    step is a frame: its other streams wait for everything enqueued on the first
+    before the step's launches, and the first waits for them after, so consecutive
+    steps never overlap (a step's launches still overlap each other)."""
+    import torch
+    streams = []
+    for go in launches:
+        if all(go.stream != s for s in streams):
+            streams.append(go.stream)
+    if len(streams) < 2:
+        def step():
+            for go in launches:
+                go()
+        return step
+    head, rest = streams[0], streams[1:]
+
+    def step():
+        ev = torch.cuda.Event()
+        ev.record(head)
+        for s_ in rest:
+            s_.wait_event(ev)
+        for go in launches:
+            go()
+        for s_ in rest:
+            e_ = torch.cuda.Event()
+            e_.record(s_)
+            head.wait_event(e_)
+    return step
+
+
 def warm(launches, warmup, min_seconds=0.3):
     """At least `warmup` steps and at least min_seconds of back-to-back launches, so
     the timed steps never run on ramping clocks (a 20-step default on 0.15 ms steps
     measured 4.8-5.3 G rays/s against 5.35 G once the clocks settle)."""
     import torch
+    step = joined(launches)
     t0, done = time.perf_counter(), 0
     while done < warmup or time.perf_counter() - t0 < min_seconds:
-        for go in launches:
-            go()
+        step()
         done += 1
         if done % 16 == 0:
             torch.cuda.synchronize()
@@ -347,7 +380,7 @@ def warm(launches, warmup, min_seconds=0.3):
 
 def time_steps(launches, steps, warmup, world):
     """Warmup, then exactly `steps` steps bracketed by barrier + synchronize; wall
-    time of the K steps. Then a probe pass on the same stream: every launch
+    time of the K steps (a multi-stream step is joined: see joined()). Then a probe pass on the same stream: every launch
     bracketed by its own HIP event pair, the mean of which is the kernel's
     average launch duration (without inter-launch gaps)."""
     import torch
@@ -355,10 +388,10 @@ def time_steps(launches, steps, warmup, world):
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
+    step = joined(launches)
     t0 = time.perf_counter()
     for _ in range(steps):
-        for go in launches:
-            go()
+        step()
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
@@ -518,11 +551,13 @@ def run_workload(name, tracer, scenes, world, rank, steps, warmup, exact, want_c
 def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact):
     """one fixed RayBuffer (the hairball diffuse frame at 8 spp,
     generated by the Renderer's <= 2^21-ray batches with their glibc seeds), cut
-    into contiguous shards; every rank traces its shard in <= 2^21-ray launches.
-    T_n = max over ranks; T_1 = rank 0 tracing the whole buffer alone, same run;
-    then the {id, t} gather to rank 0, checked against the single-GPU results."""
+    into shards — block-cyclic (STRONG["block"]-ray blocks dealt round-robin to
+    the ranks) so that every shard samples the whole frame; every rank traces its
+    shard in <= 2^21-ray launches. T_n = max over ranks; T_1 = rank 0 tracing the
+    whole buffer alone, same run; then the {id, t} gather to rank 0, checked
+    against the single-GPU results."""
     import torch
-    from mrt.dist import gather_results, shard_launches, shard_range, trace_shard
+    from mrt.dist import gather_results, local_rays, shard_launches, shard_spans
     from mrt.raygen import RAY_DIFFUSE
     from mrt.renderer import Renderer
     from mrt.tracer import RayBuffer
@@ -538,14 +573,24 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact):
     n = sum(b.size for b in parts)
     big = RayBuffer(torch.cat([b.rays for b in parts]), need_closest_hit=True)
     del parts, r
+
+    def shard_buffer(k, rk):
+        # the shard as one contiguous RayBuffer (built before the timed region: a
+        # rank generating its own rays would produce it in this order directly)
+        return RayBuffer(local_rays(big.rays, shard_spans(n, k, rk, cfg["block"])), need_closest_hit=True)
+
+    local = big if world == 1 else shard_buffer(world, rank)
     torch.cuda.synchronize()
-    lo, hi = shard_range(n, world, rank)
     # The shard's <= 2^21-ray launches are independent batches: they alternate
     # between two streams (each stream has its own trace scratch), so one
     # launch's tail overlaps the next one's start.
-    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
-    spans = shard_launches(lo, hi, cfg["max_batch"])
-    launches = [tracer.launcher(big.view(a, b), exact_rcp=exact, stream=streams[i % 2]) for i, (a, b) in enumerate(spans)]
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream()][:cfg["streams"]]
+
+    def shard_steps(buf):
+        return [tracer.launcher(buf.view(a, b), exact_rcp=exact, stream=streams[i % len(streams)])
+                for i, (a, b) in enumerate(shard_launches(0, buf.size, cfg["max_batch"], cfg["min_launches"]))]
+
+    launches = shard_steps(local)
     wall, launch_ms, _ = time_steps(launches, steps, warmup, world)
     per_rank = gather_floats(wall / steps * 1e3, world)
     tn = max(per_rank)
@@ -553,31 +598,47 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact):
     torch.cuda.synchronize()
     barrier(world)
     t0 = time.perf_counter()
-    res = big.results[lo:hi] if DIST_BACKEND == "nccl" else big.results[lo:hi].cpu()
-    full = gather_results(res, n) if world > 1 else big.results[:, :2]
+    res = local.results if DIST_BACKEND == "nccl" else local.results.cpu()
+    full = gather_results(res, n, block=cfg["block"]) if world > 1 else big.results[:, :2]
     torch.cuda.synchronize()
     gather_ms = reduce_over_ranks(1e3 * (time.perf_counter() - t0), world) if world > 1 else 0.0
     # T_1 in the same run: rank 0 alone over the whole buffer (the others wait)
     if world > 1:
         equal = None
         if rank == 0:
-            one = [tracer.launcher(big.view(a, b), exact_rcp=exact, stream=streams[i % 2])
-                   for i, (a, b) in enumerate(shard_launches(0, n, cfg["max_batch"]))]
-            w1, _, _ = time_steps(one, steps, warmup, 1)
+            w1, _, _ = time_steps(shard_steps(big), steps, warmup, 1)
             t1 = w1 / steps * 1e3
             equal = bool(torch.equal(full.to(big.results.device), big.results[:, :2]))
         barrier(world)
         t1 = reduce_over_ranks(t1 if rank == 0 else 0.0, world)
     else:
         t1, equal = tn, True
+    # One GPU, N=1: every shard the 2/4/8-rank runs would give a rank, traced alone
+    # the same way (its launches on two streams), so T_n is projected as the
+    # slowest shard and eta(n) = T_1 / (n T_n) is known before the driver's
+    # multi-GPU runs (which measure the real thing: same code, own GPU per rank).
+    projected = None
+    if world == 1:
+        projected = {}
+        for k in STRONG_PROJECT:
+            shard_ms = []
+            for r_ in range(k):
+                sb = shard_buffer(k, r_)
+                w, _, _ = time_steps(shard_steps(sb), steps, 1, 1)
+                shard_ms.append(w / steps * 1e3)
+                del sb
+            projected[str(k)] = {"tn_ms": round(max(shard_ms), 4), "eta": round(t1 / (k * max(shard_ms)), 4),
+                                 "shard_ms": [round(x, 4) for x in shard_ms]}
     return {
         "workload": cfg["name"], "rays_traced": n, "rays_counted": counted, "launch_rays_max": cfg["max_batch"],
-        "shard_rays": hi - lo, "n_gpus": world, "t1_ms": round(t1, 4), "tn_ms": round(tn, 4),
+        "shard_rays": local.size, "n_gpus": world, "t1_ms": round(t1, 4), "tn_ms": round(tn, 4),
         "per_rank_ms": [round(x, 4) for x in per_rank], "kernel_ms_per_launch": round(launch_ms, 4),
         "eta": round(t1 / (world * tn), 4), "gather_ms": round(gather_ms, 3),
         "eta_with_gather": round(t1 / (world * (tn + gather_ms)), 4),
         "value": round(counted / (tn * 1e-3) / 1e6, 2), "value_with_gather": round(counted / ((tn + gather_ms) * 1e-3) / 1e6, 2),
-        "gathered_equals_single_gpu": equal, "streams": len(streams),
+        "gathered_equals_single_gpu": equal, "streams": len(streams), "min_launches": cfg["min_launches"],
+        "shards": f"block-cyclic, {cfg['block']}-ray blocks" if cfg["block"] > 0 else "contiguous",
+        "projected_from_one_gpu": projected,
         "collective": f"{DIST_BACKEND} point-to-point gather of {n * 8} B to rank 0" if world > 1 else None,
     }
 
@@ -597,6 +658,12 @@ def main():
     ap.add_argument("--no-extra", dest="extra", action="store_false")
     ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling measurement")
     ap.add_argument("--strong-steps", type=int, default=10)
+    ap.add_argument("--strong-block", type=int, default=STRONG["block"],
+                    help="block-cyclic shard block (rays); 0 = contiguous shards")
+    ap.add_argument("--strong-streams", type=int, default=STRONG["streams"], choices=[1, 2],
+                    help="caller streams the strong-scaling launches alternate over")
+    ap.add_argument("--strong-min-launches", type=int, default=STRONG["min_launches"],
+                    help="cut every strong-scaling shard into at least this many launches")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--waves-per-cu", type=int, default=0)
     ap.add_argument("--fetch-threshold", type=int, default=-1)
@@ -646,9 +713,13 @@ def main():
                     f"cpu {r.get('cpu_baseline', {}).get('value')})")
     strong = None
     if not args.no_strong or args.scaling == "strong":
+        STRONG["min_launches"] = max(1, args.strong_min_launches)
+        STRONG["block"] = max(0, args.strong_block)
+        STRONG["streams"] = args.strong_streams
         strong = strong_scaling(tracer, scenes, world, rank, args.strong_steps, 3, exact)
         log(f"[strong] {strong['workload']} n={world}: T1 {strong['t1_ms']} ms, Tn {strong['tn_ms']} ms, "
-            f"eta {strong['eta']} (with gather {strong['eta_with_gather']})")
+            f"eta {strong['eta']} (with gather {strong['eta_with_gather']}); projected from one GPU: "
+            f"{ {k: v['eta'] for k, v in (strong['projected_from_one_gpu'] or {}).items()} }")
 
     if rank == 0:
         ref = REFERENCE_MRAYS.get(args.workload)

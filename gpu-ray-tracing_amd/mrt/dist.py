@@ -1,7 +1,8 @@
 """Multi-GPU ray sharding: the Compact2 BVH is replicated on
-every rank, the RayBuffer is split into contiguous shards, every rank traces
-its shard with its own persistent grid, and hit results are gathered to the
-root only when the caller needs them in one place.
+every rank, the RayBuffer is split into shards (contiguous ranges, or
+block-cyclic blocks so that every shard samples the whole frame), every rank
+traces its shard with its own persistent grid, and hit results are gathered to
+the root only when the caller needs them in one place.
 
 One process per GPU over torch.distributed ("nccl" = RCCL on ROCm; "gloo"
 for the CPU tests). The trace itself needs no collective.
@@ -18,6 +19,35 @@ def shard_range(n: int, world: int, rank: int) -> tuple[int, int]:
     base, extra = divmod(n, world)
     lo = rank * base + min(rank, extra)
     return lo, lo + base + (1 if rank < extra else 0)
+
+
+def shard_spans(n: int, world: int, rank: int, block: int = 0) -> list[tuple[int, int]]:
+    """The ray ranges of `rank`'s shard of n rays. block = 0: one contiguous range
+    (shard_range). block > 0: block-cyclic — the buffer cut into block-ray blocks,
+    block i to rank i % world — so every shard draws from the whole frame. A
+    frame's RayBuffer is in pixel order (AO/diffuse samples of a pixel adjacent,
+    RayGenKernels.cu:117-227), so contiguous shards are image regions of unequal
+    cost: on the hairball 1920x1080x8spp buffer the 8 contiguous shards took
+    0.59-1.12 ms on one MI355X, which caps eta(8) at 0.54."""
+    if block <= 0 or world == 1:
+        lo, hi = shard_range(n, world, rank)
+        return [(lo, hi)] if hi > lo else []
+    return [(a, min(n, a + block)) for a in range(rank * block, n, world * block)]
+
+
+def spans_index(spans, device=None) -> torch.Tensor:
+    """int64 ray indices of a list of ranges, in order."""
+    parts = [torch.arange(a, b, dtype=torch.int64, device=device) for a, b in spans]
+    return torch.cat(parts) if parts else torch.empty(0, dtype=torch.int64, device=device)
+
+
+def local_rays(rays: torch.Tensor, spans) -> torch.Tensor:
+    """The shard's rays (float32 [k, 8]) as one contiguous array (a view when the
+    shard is one range), so the rank traces it like any RayBuffer."""
+    if len(spans) == 1:
+        a, b = spans[0]
+        return rays[a:b]
+    return torch.index_select(rays, 0, spans_index(spans, rays.device))
 
 
 def replicate_buffers(bufs, src: int = 0, device=None):
@@ -47,29 +77,45 @@ def replicate_buffers(bufs, src: int = 0, device=None):
     return out
 
 
-def shard_launches(lo: int, hi: int, max_rays: int):
+def shard_launches(lo: int, hi: int, max_rays: int, min_launches: int = 1):
     """The shard [lo, hi) cut into launches of at most max_rays rays (the reference
-    traces at most 2^21 rays per launch, Renderer.cc:46)."""
-    return [(a, min(hi, a + max_rays)) for a in range(lo, hi, max_rays)]
+    traces at most 2^21 rays per launch, Renderer.cc:46). With min_launches > 1 a
+    shard is cut into at least that many launches; the cuts are balanced (sizes
+    differ by at most one ray)."""
+    n = hi - lo
+    if n <= 0:
+        return []
+    k = max(min_launches, -(-n // max_rays))
+    return [(lo + a, lo + b) for a, b in (shard_range(n, k, i) for i in range(k)) if b > a]
 
 
 def trace_shard(tracer, rays, world: int, rank: int, max_rays: int = 1 << 21, exact_rcp: bool = True,
-                stream=None):
-    """Strong-scaling step of one rank: trace its contiguous shard of the RayBuffer
-    `rays` (every rank holds the same buffer) in launches of at most max_rays rays,
-    stream-ordered, results written in place. Returns the shard's (lo, hi)."""
-    lo, hi = shard_range(rays.size, world, rank)
-    for a, b in shard_launches(lo, hi, max_rays):
-        tracer.trace_async(rays.view(a, b), exact_rcp=exact_rcp, stream=stream)
-    return lo, hi
+                stream=None, block: int = 0):
+    """Strong-scaling step of one rank: trace its shard of the RayBuffer `rays`
+    (every rank holds the same buffer) in launches of at most max_rays rays,
+    stream-ordered. block = 0: the contiguous shard, results written in place;
+    returns (lo, hi). block > 0: the block-cyclic shard, gathered into a local
+    RayBuffer first; returns that buffer (its results are the shard's, in
+    shard_spans order — what gather_results(..., block=block) expects)."""
+    if block <= 0:
+        lo, hi = shard_range(rays.size, world, rank)
+        for a, b in shard_launches(lo, hi, max_rays):
+            tracer.trace_async(rays.view(a, b), exact_rcp=exact_rcp, stream=stream)
+        return lo, hi
+    from .tracer import RayBuffer
+    local = RayBuffer(local_rays(rays.rays, shard_spans(rays.size, world, rank, block)), rays.need_closest_hit)
+    for a, b in shard_launches(0, local.size, max_rays):
+        tracer.trace_async(local.view(a, b), exact_rcp=exact_rcp, stream=stream)
+    return local
 
 
-def gather_results(local: torch.Tensor, n_total: int, dst: int = 0):
-    """Gather every rank's RayResult shard (int32 [k, 4]) to rank `dst` in ray
-    order with point-to-point send/recv (RCCL has no gather primitive; the root
-    receives from all peers at once over their direct xGMI links). Only the
-    8 useful bytes per ray (id, t) travel. Returns the full array on `dst`,
-    None elsewhere."""
+def gather_results(local: torch.Tensor, n_total: int, dst: int = 0, block: int = 0):
+    """Gather every rank's RayResult shard (int32 [k, 4], the shard's rays in
+    shard_spans order) to rank `dst` in ray order with point-to-point send/recv
+    (RCCL has no gather primitive; the root receives from all peers at once over
+    their direct xGMI links). Only the 8 useful bytes per ray (id, t) travel; a
+    block-cyclic shard arrives as one message and is scattered into place with
+    one index_copy_. Returns the full array on `dst`, None elsewhere."""
     world, rank = dist.get_world_size(), dist.get_rank()
     payload = local[:, :2].contiguous()
     if rank != dst:
@@ -77,13 +123,25 @@ def gather_results(local: torch.Tensor, n_total: int, dst: int = 0):
             dist.send(payload, dst)
         return None
     full = torch.empty((n_total, 2), dtype=torch.int32, device=local.device)
-    reqs = []
+    reqs, scatter = [], []
     for r in range(world):
-        lo, hi = shard_range(n_total, world, r)
-        if r == dst:
-            full[lo:hi].copy_(payload)
-        elif hi > lo:
-            reqs.append(dist.irecv(full[lo:hi], r))
+        spans = shard_spans(n_total, world, r, block)
+        count = sum(b - a for a, b in spans)
+        if count == 0:
+            continue
+        if len(spans) == 1:
+            lo, hi = spans[0]
+            if r == dst:
+                full[lo:hi].copy_(payload)
+            else:
+                reqs.append(dist.irecv(full[lo:hi], r))
+        else:
+            buf = payload if r == dst else torch.empty((count, 2), dtype=torch.int32, device=local.device)
+            if r != dst:
+                reqs.append(dist.irecv(buf, r))
+            scatter.append((spans_index(spans, local.device), buf))
     for q in reqs:
         q.wait()
+    for idx, buf in scatter:
+        full.index_copy_(0, idx, buf)
     return full

@@ -1,6 +1,7 @@
 """World-size-2/3 rehearsal of the multi-GPU path with gloo: the BVH is
-replicated from rank 0, rays are sharded contiguously, each rank traces its
-shard, and the results are gathered to rank 0 in ray order. On CPU the oracle
+replicated from rank 0, rays are sharded (contiguous ranges, or block-cyclic
+blocks), each rank traces its shard, and the results are gathered to rank 0 in
+ray order. On CPU the oracle
 stands in for the per-GPU tracer; the GPU test runs two ranks on one MI355X
 through the real HIP tracer (mrt.dist.trace_shard, the bench's strong-scaling
 step) and gathers with gather_results."""
@@ -13,7 +14,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from mrt.dist import shard_range
+from mrt.dist import local_rays, shard_launches, shard_range, shard_spans
 
 
 def _free_port():
@@ -24,7 +25,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, block=0):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, here)
@@ -39,9 +40,9 @@ def _worker(rank, world, port, out_path):
     nodes, woop, tri = (t.numpy() for t in replicate_buffers(bufs, src=0, device=torch.device("cpu")))
     cam, _ = scene.camera()
     rays, _ = mrt.primary_rays(cam, 61, 37)          # ragged: 2257 rays, not a multiple of the world size
-    lo, hi = shard_range(len(rays), world, rank)
-    res, _, _ = O.trace(rays[lo:hi], nodes, woop, tri)
-    full = gather_results(torch.from_numpy(res), len(rays), dst=0)
+    mine = local_rays(torch.from_numpy(rays), shard_spans(len(rays), world, rank, block)).numpy()
+    res, _, _ = O.trace(mine, nodes, woop, tri)
+    full = gather_results(torch.from_numpy(res), len(rays), dst=0, block=block)
     if rank == 0:
         want, _, _ = O.trace(rays, *mrt.Bvh.build(scene).buffers())
         np.save(out_path, np.stack([full.numpy()[:, 0], want[:, 0], full.numpy()[:, 1], want[:, 1]]))
@@ -49,12 +50,37 @@ def _worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_replicate_shard_gather(tmp_path, world):
+@pytest.mark.parametrize("world,block", [(2, 0), (3, 0), (2, 100), (3, 64)])
+def test_replicate_shard_gather(tmp_path, world, block):
+    """block 0: contiguous shards; block > 0: block-cyclic shards (a ragged last block)."""
     out = str(tmp_path / "res.npy")
-    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), out, block), nprocs=world, join=True)
     a = np.load(out)
     assert np.array_equal(a[0], a[1]) and np.array_equal(a[2], a[3])
+
+
+def test_block_cyclic_spans_partition():
+    """Every ray in exactly one shard; blocks dealt round-robin; shard sizes within one block."""
+    for n in (0, 1, 99, 100, 101, 16588800):
+        for w in (1, 2, 3, 8):
+            for block in (1, 100, 1 << 14):
+                spans = [shard_spans(n, w, r, block) for r in range(w)]
+                flat = sorted(s for sp in spans for s in sp)
+                assert sum(b - a for a, b in flat) == n
+                assert all(flat[i][1] == flat[i + 1][0] for i in range(len(flat) - 1))
+                if n and w > 1:
+                    assert all(a // block % w == r for r, sp in enumerate(spans) for a, _ in sp)
+                sizes = [sum(b - a for a, b in sp) for sp in spans]
+                assert max(sizes) - min(sizes) <= max(block, 1)
+
+
+def test_shard_launches_balanced():
+    assert shard_launches(0, 16588800, 1 << 21) == [(i * 2073600, (i + 1) * 2073600) for i in range(8)]
+    assert shard_launches(100, 2073700, 1 << 21, 2) == [(100, 1036900), (1036900, 2073700)]
+    assert shard_launches(5, 5, 10) == []
+    spans = shard_launches(0, 12345, 1000, 3)
+    assert len(spans) == 13 and spans[0][0] == 0 and spans[-1][1] == 12345
+    assert max(b - a for a, b in spans) <= 1000
 
 
 def test_shard_ranges_partition():
@@ -88,9 +114,9 @@ def _gpu_worker(rank, world, port, out_path):
     prim, _ = gen.primary(cam, 173, 91)
     tracer.trace_batch(prim, exact_rcp=True)
     rays = gen.ao(prim, 3, cam.far, closest_hit=True)   # one fixed RayBuffer, identical on every rank
-    lo, hi = trace_shard(tracer, rays, world, rank, max_rays=4096)   # several launches per shard
+    local = trace_shard(tracer, rays, world, rank, max_rays=4096, block=1000)   # block-cyclic, several launches
     torch.cuda.synchronize()
-    full = gather_results(rays.results[lo:hi].cpu(), rays.size, dst=0)
+    full = gather_results(local.results.cpu(), rays.size, dst=0, block=1000)
     if rank == 0:
         np.save(out_path + ".rays.npy", rays.rays.cpu().numpy())
         np.save(out_path + ".res.npy", full.numpy())
@@ -103,7 +129,8 @@ def _gpu_worker(rank, world, port, out_path):
 @pytest.mark.gpu
 def test_two_ranks_on_one_gpu_trace_shards_and_gather(tmp_path):
     """Two gloo ranks sharing one MI355X: replicate -> shard (strong scaling: one fixed
-    RayBuffer, contiguous shards, <= 4096-ray launches) -> HIP trace -> gather to rank 0;
+    RayBuffer, block-cyclic shards of 1000-ray blocks, <= 4096-ray launches) -> HIP
+    trace -> gather to rank 0;
     the gathered {id, t} equal the oracle over the whole buffer."""
     import oracle_lib as O
     if not torch.cuda.is_available():
