@@ -36,9 +36,16 @@ def shard_spans(n: int, world: int, rank: int, block: int = 0) -> list[tuple[int
 
 
 def spans_index(spans, device=None) -> torch.Tensor:
-    """int64 ray indices of a list of ranges, in order."""
-    parts = [torch.arange(a, b, dtype=torch.int64, device=device) for a, b in spans]
-    return torch.cat(parts) if parts else torch.empty(0, dtype=torch.int64, device=device)
+    """int64 ray indices of a list of ranges, in order (a handful of kernels
+    whatever the number of ranges: a block-cyclic shard has hundreds)."""
+    if not spans:
+        return torch.empty(0, dtype=torch.int64, device=device)
+    starts = torch.tensor([a for a, _ in spans], dtype=torch.int64, device=device)
+    lens = torch.tensor([b - a for a, b in spans], dtype=torch.int64, device=device)
+    first = torch.cumsum(lens, 0) - lens                    # position of each range's first index
+    total = int(sum(b - a for a, b in spans))
+    pos = torch.arange(total, dtype=torch.int64, device=device)
+    return torch.repeat_interleave(starts - first, lens, output_size=total) + pos
 
 
 def local_rays(rays: torch.Tensor, spans) -> torch.Tensor:
