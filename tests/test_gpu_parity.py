@@ -338,6 +338,84 @@ def test_ragged_batch_sizes(tracer, n):
     assert np.array_equal(res[:, :2], want[:n, :2])
 
 
+def special_rays(base, seed=7):
+    """Rays with the values a caller can hand the kernel without meaning to: axis-parallel
+    directions with +-0 components (the 2^-80 clamp keeps the zero's sign), a zero
+    direction, denormal components (flushed), NaN / inf components, tmin > tmax,
+    tmin == tmax, a huge negative tmin, tmax = inf / NaN, origins 1e30 away, and rays
+    starting exactly on their own first hit point. Built from primary rays `base`."""
+    rng = np.random.default_rng(seed)
+    k = 192
+    sel = rng.choice(len(base), k)
+    o, tmin, d, tmax = base[sel, 0:3], base[sel, 3], base[sel, 4:7], base[sel, 7]
+    groups = []
+
+    def add(o_=None, tmin_=None, d_=None, tmax_=None):
+        r = np.empty((k, 8), np.float32)
+        r[:, 0:3] = o if o_ is None else o_
+        r[:, 3] = tmin if tmin_ is None else tmin_
+        r[:, 4:7] = d if d_ is None else d_
+        r[:, 7] = tmax if tmax_ is None else tmax_
+        groups.append(r)
+
+    for axis in range(3):
+        dd = np.zeros((k, 3), np.float32)
+        dd[:, axis] = np.where(rng.random(k) < 0.5, 1.0, -1.0)
+        dd[k // 2:, (axis + 1) % 3] = -0.0
+        add(d_=dd)
+    add(d_=np.zeros((k, 3), np.float32))
+    dd = d.copy()
+    dd[:, 0] = np.float32(1e-40)
+    dd[: k // 2, 1] = np.float32(-3e-39)
+    add(d_=dd)
+    for j in range(3):
+        oo = o.copy()
+        oo[:, j] = np.nan
+        add(o_=oo)
+        dd = d.copy()
+        dd[:, j] = np.nan
+        add(d_=dd)
+        dd = d.copy()
+        dd[:, j] = np.where(rng.random(k) < 0.5, np.inf, -np.inf)
+        add(d_=dd)
+    add(tmin_=tmax + 1.0)
+    add(tmin_=tmax)
+    add(tmin_=np.full(k, -1e30, np.float32))
+    add(tmax_=np.full(k, np.inf, np.float32))
+    add(tmax_=np.full(k, np.nan, np.float32))
+    add(tmin_=np.full(k, np.nan, np.float32))
+    add(o_=(o - d * np.float32(1e30)).astype(np.float32))
+    return np.concatenate(groups)
+
+
+@pytest.mark.parametrize("scene", ["bunny", "hairball:800", "sponza"])
+def test_special_value_rays(tracer, scene):
+    """Edge-value rays (special_rays) traced against the oracle: the per-lane order walks
+    the same Compact2 nodes with the same arithmetic, so id, t and the counters are
+    bit-identical whatever the values; the speculative 4-wide mode gives the same
+    closest hits and the same any-hit hit/miss."""
+    bufs, base, _, _, _ = scene_setup(scene, 64, 48, "primary")
+    rays = special_rays(base)
+    # rays that start on their first hit point (t of the hit along the ray, tmin 0)
+    prim, _, _ = O.trace(base, *bufs)
+    hit = np.nonzero(prim[:, 0] >= 0)[0][:192]
+    on = base[hit].copy()
+    on[:, 0:3] = on[:, 0:3] + on[:, 4:7] * prim[hit, 1].view(np.float32)[:, None]
+    on[:, 3] = 0.0
+    rays = np.concatenate([rays, on.astype(np.float32)])
+    for any_hit in (False, True):
+        want, st, _ = O.trace(rays, *bufs, any_hit=any_hit, stats=True)
+        res, gst = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=False, stats=True)
+        assert np.array_equal(res[:, :2], want[:, :2]), f"per-lane order, any_hit={any_hit}"
+        assert np.array_equal(gst[:, :3], st[:, :3]), f"per-lane counters, any_hit={any_hit}"
+        res, _ = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=True)
+        if any_hit:
+            assert np.array_equal(res[:, 0] == -1, want[:, 0] == -1), "speculative any-hit hit/miss"
+        else:
+            bad = np.nonzero((res[:, 0] != want[:, 0]) | (res[:, 1] != want[:, 1]))[0]
+            assert len(bad) == 0, f"speculative closest hit differs on rays {bad[:8]} (of {len(rays)})"
+
+
 def test_empty_batch_returns_zero_ms(tracer):
     from mrt.tracer import GpuBvh, RayBuffer
     tracer.set_bvh(GpuBvh(kat.scene_two_floors()))
