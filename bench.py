@@ -418,6 +418,9 @@ def gather_to_root(batches, world):
     (mrt/dist.py). Returns (ms, bytes received by rank 0)."""
     import torch
     from mrt.dist import gather_results
+    # one untimed pass first: RCCL creates its point-to-point communicators on first use
+    for rb, _ in batches.batches:
+        gather_results(rb.results if DIST_BACKEND == "nccl" else rb.results.cpu(), world * rb.size)
     torch.cuda.synchronize()
     barrier(world)
     t0 = time.perf_counter()
@@ -594,7 +597,10 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact):
     wall, launch_ms, _ = time_steps(launches, steps, warmup, world)
     per_rank = gather_floats(wall / steps * 1e3, world)
     tn = max(per_rank)
-    # gather of this shard's {id, t} to rank 0 (RCCL point-to-point; gloo: via host)
+    # gather of this shard's {id, t} to rank 0 (RCCL point-to-point; gloo: via host),
+    # after one untimed gather (RCCL creates its point-to-point communicators on first use)
+    if world > 1:
+        gather_results(local.results if DIST_BACKEND == "nccl" else local.results.cpu(), n, block=cfg["block"])
     torch.cuda.synchronize()
     barrier(world)
     t0 = time.perf_counter()
