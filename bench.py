@@ -495,7 +495,8 @@ def roofline(name, alg_bytes_per_launch, kernel_ms, bvh_bytes):
 # cfg.autotune candidates (csrc/mrt_api.cpp tune_candidate)
 SCHEDULES = {0: "static rounds, 20 waves/CU", 1: "static rounds, 8 waves/CU", 2: "8 per-XCD queues",
              3: "global queue, refill at 48, 16 waves/CU", 4: "global queue, refill at 48, 12 waves/CU",
-             5: "static rounds, 16 waves/CU", 6: "static rounds, 12 waves/CU"}
+             5: "static rounds, 16 waves/CU", 6: "static rounds, 12 waves/CU",
+             7: "8 per-XCD queues, spec_slack 4"}
 
 
 def run_workload(name, tracer, scenes, world, rank, steps, warmup, exact, want_cpu):

@@ -66,7 +66,7 @@ struct mrt_tracer {
 
 // Launch-schedule autotuning state of one (batch size, kernel variant).
 struct TuneState {
-    static constexpr int kCandidates = 7;
+    static constexpr int kCandidates = 8;
     static constexpr int kSamples = 4;   // timed launches per candidate (the minimum counts)
     int launches = 0;    // exploring launches so far (the first round of candidates runs untimed:
                          // the clocks and caches are still settling)
@@ -341,7 +341,7 @@ int refresh_wide(mrt_tracer* t) {
 // cache residency (profiles/round2_tuning.md: static rounds, fewer waves, per-XCD
 // queues and the global queue each win somewhere by 5-70 %). With cfg.autotune
 // and the distribution knobs at their defaults, the first launches of a batch
-// size cycle through these seven candidates, each timed with an event pair that is
+// size cycle through these eight candidates, each timed with an event pair that is
 // read back on a later launch (never blocking), and after kSamples launches each
 // the fastest is kept for that batch size. Results do not depend on the schedule
 // (closest hits are the same hits; an any-hit ray may report a different valid hit).
@@ -359,7 +359,11 @@ mrt_launch_cfg tune_candidate(const mrt_launch_cfg& base, int c) {
         case 3: x.num_queues = 1; x.fetch_threshold = 48; x.waves_per_cu = 16; break;   // global queue
         case 4: x.num_queues = 1; x.fetch_threshold = 48; x.waves_per_cu = 12; break;
         case 5: x.waves_per_cu = 16; break;
-        default: x.waves_per_cu = 12; break;
+        case 6: x.waves_per_cu = 12; break;
+        default:   // per-XCD queues, the wave leaving for its leaves once <= 4 lanes still search
+            x.num_queues = 8;
+            if (base.spec_slack == kDefaultSpecSlack) x.spec_slack = 4;
+            break;
     }
     return x;
 }

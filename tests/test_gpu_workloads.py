@@ -140,7 +140,7 @@ def test_automatic_launch_config(env, name, queues, waves):
 
 
 def test_autotuned_schedule_settles_and_keeps_results(env):
-    """cfg.autotune (default): the first launches of a batch size cycle through seven
+    """cfg.autotune (default): the first launches of a batch size cycle through eight
     ray-distribution schedules, timed without blocking, then keep the fastest. Every
     launch, exploring or settled, returns the oracle's closest hits."""
     bench, scenes, tracer, threads = env
@@ -158,5 +158,5 @@ def test_autotuned_schedule_settles_and_keeps_results(env):
         seen.add(tracer.last_info["autotune_candidate"])
         got = rb.results_numpy()
         assert np.array_equal(got[:, :2], want[:, :2]), f"launch {i} (candidate {tracer.last_info['autotune_candidate']})"
-    assert seen == set(range(7)) or tracer.last_info["autotune_locked"] == 1
+    assert seen == set(range(8)) or tracer.last_info["autotune_locked"] == 1
     assert tracer.last_info["autotune_locked"] == 1
