@@ -496,7 +496,8 @@ def roofline(name, alg_bytes_per_launch, kernel_ms, bvh_bytes):
 SCHEDULES = {0: "static rounds, 20 waves/CU", 1: "static rounds, 8 waves/CU", 2: "8 per-XCD queues",
              3: "global queue, refill at 48, 16 waves/CU", 4: "global queue, refill at 48, 12 waves/CU",
              5: "static rounds, 16 waves/CU", 6: "static rounds, 12 waves/CU",
-             7: "8 per-XCD queues, spec_slack 4"}
+             7: "8 per-XCD queues, spec_slack 4",
+             8: "the best of 0-7 with spec_slack 4", 9: "the best of 0-7 with spec_slack 6"}
 
 
 def run_workload(name, tracer, scenes, world, rank, steps, warmup, exact, want_cpu):

@@ -66,14 +66,18 @@ struct mrt_tracer {
 
 // Launch-schedule autotuning state of one (batch size, kernel variant).
 struct TuneState {
-    static constexpr int kCandidates = 8;
+    // Stage 1: kSchedules ray-distribution schedules; stage 2: the stage-1 winner
+    // with the speculation slack at 4 and 6 (candidates kSchedules, kSchedules + 1).
+    static constexpr int kSchedules = 8;
+    static constexpr int kCandidates = kSchedules + 2;
     static constexpr int kSamples = 4;   // timed launches per candidate (the minimum counts)
     int launches = 0;    // exploring launches so far (the first round of candidates runs untimed:
                          // the clocks and caches are still settling)
     float best[kCandidates];
     int samples[kCandidates] = {};
     int next = 0;        // candidate the next exploring launch uses
-    int locked = -1;     // the chosen candidate, once every one has kSamples samples
+    int stage1 = -1;     // the stage-1 winner, once every schedule has kSamples samples
+    int locked = -1;     // the chosen candidate, once stage 2's have kSamples samples too
     void* stream = nullptr;          // the stream this batch size was first launched on
     bool multiStream = false;        // launched on several streams: keeps the fixed rule
     struct Pending {
@@ -347,7 +351,14 @@ int refresh_wide(mrt_tracer* t) {
 // (closest hits are the same hits; an any-hit ray may report a different valid hit).
 constexpr int kMaxTuned = 64;   // batch sizes tuned per handle; others use the rule
 
-mrt_launch_cfg tune_candidate(const mrt_launch_cfg& base, int c) {
+mrt_launch_cfg tune_candidate(const mrt_launch_cfg& base, int c, int stage1) {
+    if (c >= TuneState::kSchedules) {
+        // stage 2: the stage-1 winner, the wave turning to its leaves once <= 4 (6) lanes
+        // still search (only when the caller left spec_slack at its default)
+        mrt_launch_cfg x = tune_candidate(base, stage1, stage1);
+        if (base.spec_slack == kDefaultSpecSlack) x.spec_slack = c == TuneState::kSchedules ? 4 : 6;
+        return x;
+    }
     mrt_launch_cfg x = base;
     x.fetch_threshold = 0;
     x.waves_per_cu = 0;
@@ -379,10 +390,20 @@ void tune_collect(TuneState* st) {
         p.cand = -1;
     }
     if (st->locked >= 0) return;
-    for (int c = 0; c < TuneState::kCandidates; c++)
+    if (st->stage1 < 0) {
+        for (int c = 0; c < TuneState::kSchedules; c++)
+            if (st->samples[c] < TuneState::kSamples) return;
+        int best = 0;
+        for (int c = 1; c < TuneState::kSchedules; c++)
+            if (st->best[c] < st->best[best]) best = c;
+        st->stage1 = best;
+        st->next = TuneState::kSchedules;
+        return;
+    }
+    for (int c = TuneState::kSchedules; c < TuneState::kCandidates; c++)
         if (st->samples[c] < TuneState::kSamples) return;
-    int best = 0;
-    for (int c = 1; c < TuneState::kCandidates; c++)
+    int best = st->stage1;
+    for (int c = TuneState::kSchedules; c < TuneState::kCandidates; c++)
         if (st->best[c] < st->best[best]) best = c;
     st->locked = best;
 }
@@ -450,8 +471,9 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
             cand = tune->locked;
         } else {
             cand = tune->next;
-            tune->next = (tune->next + 1) % TuneState::kCandidates;
-            if (tune->launches++ >= TuneState::kCandidates)
+            tune->next = tune->stage1 < 0 ? (tune->next + 1) % TuneState::kSchedules
+                                          : TuneState::kSchedules + (tune->next + 1 - TuneState::kSchedules) % 2;
+            if (tune->launches++ >= TuneState::kSchedules)
                 for (auto& p : tune->pending)
                     if (p.cand < 0) {
                         slot = &p;
@@ -462,7 +484,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
                 MRT_HIP(hipEventCreate(&slot->stop));
             }
         }
-        cfg = tune_candidate(cfg, cand);
+        cfg = tune_candidate(cfg, cand, tune->stage1);
     }
     const int blocks = grid_blocks(t, cfg, v, numRays, &perCU);
     const int totalLanes = blocks * mrt::kBlockThreads;

@@ -95,7 +95,8 @@ typedef struct mrt_launch_cfg {
     int32_t autotune;          /* 1 = with the distribution knobs above at their defaults, the first launches
                                   of each batch size (per kernel variant, up to 64 sizes) time eight ray-
                                   distribution schedules (static rounds at 20, 16, 12 or 8 waves/CU, per-XCD
-                                  queues with spec_slack 2 or 4, the global queue at 16 or 12 waves/CU) four
+                                  queues with spec_slack 2 or 4, the global queue at 16 or 12 waves/CU), then
+                                  the winner with spec_slack 4 and 6 (when left at its default), four
                                   times each without
                                   blocking, after one untimed round of them, and keep the fastest (a batch size launched on more than one stream keeps the
                                   fixed rule); reset by bind and set_config (default 1). 0 = the fixed
@@ -114,7 +115,7 @@ typedef struct mrt_trace_info {
     int32_t stack_overflows;   /* pushes past the 64-entry stack in this launch (then the call returns
                                   MRT_ERR_STACK_OVERFLOW; 0 for any SBVH of depth <= 64)            */
     int32_t node_bytes;        /* bytes per node the launch read: 64 (Compact2 or quantized 4-wide), 128 */
-    int32_t autotune_candidate; /* cfg.autotune: the schedule candidate this launch used (0..7), else -1 */
+    int32_t autotune_candidate; /* cfg.autotune: the schedule candidate this launch used (0..9), else -1 */
     int32_t autotune_locked;   /* 1 once the batch size's schedule is chosen                      */
 } mrt_trace_info;
 

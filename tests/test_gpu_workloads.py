@@ -141,8 +141,9 @@ def test_automatic_launch_config(env, name, queues, waves):
 
 def test_autotuned_schedule_settles_and_keeps_results(env):
     """cfg.autotune (default): the first launches of a batch size cycle through eight
-    ray-distribution schedules, timed without blocking, then keep the fastest. Every
-    launch, exploring or settled, returns the oracle's closest hits."""
+    ray-distribution schedules, timed without blocking, then the winner with the
+    speculation slack at 4 and 6, and keep the fastest. Every launch, exploring or
+    settled, returns the oracle's closest hits."""
     bench, scenes, tracer, threads = env
     name = "bunny-primary-1024x768"
     e = scenes.get(bench.workload_spec(name)[0])
@@ -153,10 +154,10 @@ def test_autotuned_schedule_settles_and_keeps_results(env):
     tracer.set_config(autotune=1)   # a fresh tuning state for this handle
     want, _, _ = O.trace(rb.rays.cpu().numpy(), *bufs, threads=threads)
     seen = set()
-    for i in range(60):
+    for i in range(90):
         tracer.trace_batch(rb, exact_rcp=True)   # blocking: every launch's timing is read back by the next
         seen.add(tracer.last_info["autotune_candidate"])
         got = rb.results_numpy()
         assert np.array_equal(got[:, :2], want[:, :2]), f"launch {i} (candidate {tracer.last_info['autotune_candidate']})"
-    assert seen == set(range(8)) or tracer.last_info["autotune_locked"] == 1
+    assert seen == set(range(10))
     assert tracer.last_info["autotune_locked"] == 1
