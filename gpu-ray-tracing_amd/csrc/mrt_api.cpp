@@ -346,8 +346,9 @@ int refresh_wide(mrt_tracer* t) {
 // queues and the global queue each win somewhere by 5-70 %). With cfg.autotune
 // and the distribution knobs at their defaults, the first launches of a batch
 // size cycle through these eight candidates, each timed with an event pair that is
-// read back on a later launch (never blocking), and after kSamples launches each
-// the fastest is kept for that batch size. Results do not depend on the schedule
+// read back on a later launch (never blocking); after kSamples launches each the
+// fastest is timed again with the speculation slack at 4 and 6 (stage 2), and the
+// fastest of the three is kept for that batch size. Results do not depend on the schedule
 // (closest hits are the same hits; an any-hit ray may report a different valid hit).
 constexpr int kMaxTuned = 64;   // batch sizes tuned per handle; others use the rule
 
