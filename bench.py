@@ -45,9 +45,16 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "gpu-ray-tracing_amd"))
 
 METRIC = "Mrays/s (primary/AO/diffuse) at 1/2/4/8 GPUs; achieved HBM GB/s % of peak"
-HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
-MALL_BYTES = 256 << 20  # Infinity Cache: a BVH above this streams from HBM
-PROFILE_TAG = "round2"  # committed rocprofv3 summaries this line cites (profiles/<tag>_<workload>_*)
+# Ceilings of the cache levels the trace's bytes are served from (MI355X_MICROARCH.md):
+HBM_PEAK_GBS = 8000.0    # HBM3E peak (chip-level parameters, §HBM)
+MALL_PEAK_GBS = 8600.0   # Infinity Cache, uniformly random rows (§Indexed rows, 38 MB table)
+L2_PEAK_GBS = 34500.0    # the eight XCD L2s together (§L2)
+LINE_BYTES = 128         # gfx950 L1 and L2 line: one TCP_TCC_READ_REQ / TCC_EA0_RDREQ per line
+                         # (tools/ubench_levels.hip, profiles/round3_counter_calibration.md)
+MALL_BYTES = 256 << 20   # Infinity Cache: a BVH above this streams from HBM
+PROFILE_TAG = "round3"   # committed rocprofv3 summaries this line cites (profiles/<tag>_<workload>_*)
+STORE = None             # mrt.schedules.ScheduleStore the tracer's schedules are locked from (main())
+LEARNED = None           # ScheduleStore collecting the schedules this run settled (--save-schedules)
 
 # README numbers (Kepler-class sm_35 build, hardware unstated) — README.md:46-81.
 REFERENCE_MRAYS = {
@@ -107,19 +114,21 @@ def workload_spec(name):
     return (scene, w, h, kind.rstrip("0123456789"), bounces)
 
 
-def pmc_profile(name):
-    """rocprofv3 PMC summary of a workload (FETCH_SIZE / WRITE_SIZE in separate
-    passes, tools/profile_round.sh + tools/summarize_prof.py): counters cannot be
-    read inside this timed process, so the committed profile is cited."""
-    for tag in (PROFILE_TAG, "round1"):
-        path = os.path.join("profiles", f"{tag}_{name}_pmc_summary.json")
-        if os.path.exists(os.path.join(REPO, path)):
-            with open(os.path.join(REPO, path)) as f:
-                s = json.load(f)
-            hbm = s.get("hbm_bytes_per_launch")
-            if hbm:
-                return int(hbm["total_corrected"]), s.get("avg_ns"), path
-    return None, None, None
+def pmc_profile(name, rcp="exact"):
+    """rocprofv3 PMC summary of a workload (one counter group per pass,
+    tools/profile_round.sh + tools/summarize_prof.py): counters cannot be read
+    inside this timed process, so the committed profile of the same command is
+    cited. Per launch: bytes the L1s requested from L2 (TCP_TCC_READ_REQ lines),
+    bytes L2 read over the fabric (TCC_EA0_RDREQ lines: Infinity Cache or HBM) and
+    wrote (WRITE_SIZE), the mean kernel duration and the schedule it ran."""
+    tag = "" if rcp == "exact" else "_rcpfast"
+    path = os.path.join("profiles", f"{PROFILE_TAG}_{name}{tag}_pmc_summary.json")
+    if not os.path.exists(os.path.join(REPO, path)):
+        return None
+    with open(os.path.join(REPO, path)) as f:
+        s = json.load(f)
+    s["path"] = path
+    return s
 
 
 def log(*a):
@@ -221,6 +230,7 @@ class SceneCache:
         if scene_name in self.entries:
             return self.entries[scene_name]
         import mrt
+        from mrt.schedules import bvh_fingerprint
         from mrt.tracer import GpuBvh
         scene = mrt.Scene.synthetic(scene_name, 0, 1)
         t0 = time.perf_counter()
@@ -244,6 +254,7 @@ class SceneCache:
             from mrt.dist import replicate_buffers
             bufs = tuple(replicate_buffers(bufs, src=0))
         gbvh = GpuBvh(bufs)   # device tensors from RCCL are bound in place; gloo/numpy are uploaded
+        gbvh.fingerprint = bvh_fingerprint(*bufs)   # the key of the BVH's saved schedules (mrt/schedules.py)
         entry = {"scene": scene, "gbvh": gbvh, "stats": stats, "build_s": build_s, "cached": cached,
                  "host_bufs": bufs if self.rank == 0 and self.world == 1 else None}
         self.entries[scene_name] = entry
@@ -278,6 +289,15 @@ def mrt_seed(bounce):
     return mrt.AO_SEED + bounce
 
 
+def bind(tracer, gbvh):
+    """set_bvh, then lock the BVH's saved schedules (bind forgets them). Returns the
+    bind's wall ms (wide-node derivation included) and how many schedules were locked."""
+    tracer.set_bvh(gbvh)
+    ms = tracer.bind_info()["bind_ms"]
+    n = STORE.apply(tracer, gbvh.fingerprint) if STORE is not None else 0
+    return ms, n
+
+
 class Batches:
     """Ray batches of one workload, generated on the device like the reference
     Renderer (Renderer.cc:112-152,242-291; RayGen.cc:50-120): primary rays in
@@ -289,7 +309,7 @@ class Batches:
         from mrt.raygen import DeviceRayGen
         sname, w, h, kind, bounces = workload_spec(name)
         self.name, self.kind, self.w, self.h = name, kind, w, h
-        tracer.set_bvh(gbvh)
+        self.bind_ms, self.locked_from_store = bind(tracer, gbvh)
         cam, ao_radius = scene.camera()
         gen = DeviceRayGen(scene)   # RayGen on the device (mrt_raygen_*), like the reference's RayGenKernels
         prim, _ = gen.primary(cam, w, h, subpixel=subpixel_sample(rank))
@@ -399,6 +419,7 @@ def time_steps(launches, steps, warmup, world):
     probe = max(3, min(steps, 50))
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(probe * len(launches))]
+    one_stream = all(go.stream == launches[0].stream for go in launches)
     k = 0
     for _ in range(probe):
         for go in launches:
@@ -406,7 +427,8 @@ def time_steps(launches, steps, warmup, world):
             go()
             ev[k][1].record(go.stream)
             k += 1
-            torch.cuda.synchronize()   # one launch at a time: its own duration, not an overlap
+            if not one_stream:
+                torch.cuda.synchronize()   # one launch at a time: its own duration, not an overlap
     torch.cuda.synchronize()
     per_launch = [a.elapsed_time(b) for a, b in ev]
     return wall, float(np.mean(per_launch)), warmed
@@ -435,19 +457,23 @@ def gather_to_root(batches, world):
     return reduce_over_ranks(ms, world), nbytes
 
 
-def cpu_baseline(batches, bufs, counted, threads, label):
+def cpu_baseline(batches, bufs, counted, threads, label, fast_results=None):
     """The oracle (oracle/, a scalar C restatement of the same traversal, one ray at a
     time, std::thread-style dynamic chunks) on the host cores over every batch of the
     workload: best of 5 after 1 warmup. Also checks the GPU results against it
-    (parity on the bench input: closest hit bit-identical, any hit hit/miss-identical)."""
+    (parity on the bench input: closest hit bit-identical, any hit hit/miss-identical)
+    and, given the fast-reciprocal mode's results, classifies their mismatches
+    (SURVEY §8(a) Note 3: tie / edge / other, tests/oracle_lib.classify_fast_rcp)."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib as O
     nodes, woop, tri = bufs
     host = [(rb.rays.cpu().numpy(), not rb.need_closest_hit, rb.results_numpy()) for rb, _ in batches]
     secs, agree, n = [], 0, 0
+    fast = {"rays": 0, "mismatch": 0, "tie": 0, "edge": 0, "other": 0, "any_hit_outcome_flips": 0} \
+        if fast_results is not None else None
     for rep in range(6):
         total = 0.0
-        for rays, any_hit, gpu in host:
+        for b, (rays, any_hit, gpu) in enumerate(host):
             res, _, s = O.trace(rays, nodes, woop, tri, any_hit=any_hit, threads=threads)
             total += s
             if rep == 0:
@@ -455,52 +481,128 @@ def cpu_baseline(batches, bufs, counted, threads, label):
                     (gpu[:, 0] == res[:, 0]) & (gpu[:, 1] == res[:, 1])
                 agree += int(same.sum())
                 n += len(rays)
+                if fast is not None:
+                    fr = fast_results[b]
+                    fast["rays"] += len(rays)
+                    if any_hit:
+                        fast["any_hit_outcome_flips"] += int(((fr[:, 0] == -1) != (res[:, 0] == -1)).sum())
+                    else:
+                        c = O.classify_fast_rcp(rays, fr, res, woop, tri)
+                        for k in ("mismatch", "tie", "edge", "other"):
+                            fast[k] += c[k]
         if rep:
             secs.append(total)
     best = min(secs)
     rays = sum(len(r) for r, _, _ in host)
-    return {"value": round(counted / best / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(), "seconds_best": round(best, 4),
-            "sample": f"{label}: all {len(host)} batch(es), {rays} rays ({counted} counted), best of 5 after 1 "
-                      f"warmup, {threads} threads, oracle/trace_oracle.c (same Compact2 bytes, same rays)",
-            "parity_exact_fraction": round(agree / max(1, n), 6)}
-
-
-def roofline(name, alg_bytes_per_launch, kernel_ms, bvh_bytes):
-    """achieved = algorithmic bytes per launch / average kernel
-    duration; traffic = PMC-measured HBM bytes per launch (committed rocprofv3
-    summary) and the HBM rate they imply. bound: the BVH of a cache-resident scene
-    never leaves the 256 MB MALL/L2 (algorithmic GB/s can then exceed the HBM
-    peak), so the kernel is latency-bound; only a BVH above the MALL streams from HBM,
-    and even there the measured traffic rate is what the HBM fraction is."""
-    traffic, prof_ns, src = pmc_profile(name)
-    achieved = alg_bytes_per_launch / (kernel_ms * 1e-3) / 1e9
-    out = {"bound": "latency", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-           "algorithmic_bytes_per_launch": int(alg_bytes_per_launch), "kernel_ms": round(kernel_ms, 4),
-           "bvh_bytes": int(bvh_bytes), "bvh_exceeds_mall": bvh_bytes > MALL_BYTES}
-    if traffic:
-        hbm = traffic / (kernel_ms * 1e-3) / 1e9
-        out.update({"hbm_measured_GBps": round(hbm, 1), "hbm_measured_frac": round(hbm / HBM_PEAK_GBS, 4),
-                    "traffic_source": src,
-                    "profile_kernel_ms": round(prof_ns / 1e6, 4) if prof_ns else None})
-        if hbm > 0.5 * HBM_PEAK_GBS:
-            out["bound"] = "hbm"
-    out["bound_basis"] = ("measured HBM traffic near peak" if out["bound"] == "hbm" else
-                          "dependent node->node fetch chains; measured HBM rate well below peak"
-                          if traffic else "cache-resident BVH; dependent fetch chains (no PMC profile cited)")
+    out = {"value": round(counted / best / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+           "cpu_model": cpu_model(), "seconds_best": round(best, 4),
+           "sample": f"{label}: all {len(host)} batch(es), {rays} rays ({counted} counted), best of 5 after 1 "
+                     f"warmup, {threads} threads, oracle/trace_oracle.c (same Compact2 bytes, same rays)",
+           "parity_exact_fraction": round(agree / max(1, n), 6)}
+    if fast is not None:
+        fast["tie_fraction"] = round(fast["tie"] / max(1, fast["rays"]), 8)
+        out["rcp_fast_parity"] = fast
     return out
+
+
+def roofline(name, alg_bytes_per_launch, kernel_ms, bvh_bytes, schedule, rcp="exact"):
+    """Per-level roofline of the dominant kernel. The trace's bytes
+    are served by three levels, each priced against its own ceiling:
+      l2      lines the L1s fetched from L2 (TCP_TCC_READ_REQ x 128 B) / 34.5 TB/s;
+      fabric  lines L2 fetched over the fabric (TCC_EA0_RDREQ x 128 B) + WRITE_SIZE,
+              served by the Infinity Cache or HBM / 8.6 TB/s (the Infinity Cache's
+              random-row rate, above HBM's 8 TB/s, so the bound holds whichever serves them);
+    frac = the larger of the two fractions, `bound` names that level, `achieved` /
+    `peak` are its rate and ceiling, `traffic` = the fabric bytes per launch (an upper
+    bound on HBM bytes: Infinity-Cache hits are counted too) and hbm_measured_frac =
+    traffic / kernel time / 8 TB/s. Rates use this run's kernel time (HIP events);
+    the cited profile must have run the same schedule (autotune candidate and grid)
+    or no level is priced. The algorithmic bytes of SURVEY.md §8(d) (every byte the
+    rays read, cache hits included) are reported beside it, as a rate only: they are
+    not bounded by any one level."""
+    alg = alg_bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+    out = {"bound": None, "achieved": None, "peak": None, "unit": "GB/s", "frac": None, "traffic": None,
+           "kernel_ms": round(kernel_ms, 4), "bvh_bytes": int(bvh_bytes), "bvh_exceeds_mall": bvh_bytes > MALL_BYTES,
+           "algorithmic": {"bytes_per_launch": int(alg_bytes_per_launch), "GBps": round(alg, 1),
+                           "note": "SURVEY §8(d) bytes incl. L1/L2 hits; not a level's traffic"}}
+    prof = pmc_profile(name, rcp)
+    if prof is None:
+        out["note"] = "no committed PMC profile for this workload"
+        return out
+    want = {k: schedule.get(k) for k in ("autotune_candidate", "grid_waves", "num_queues", "fetch_threshold")}
+    got = {k: (prof.get("schedule") or {}).get(k) for k in want}
+    out["profile"] = {"path": prof["path"], "kernel_ms": round(prof["avg_ns"] / 1e6, 4),
+                      "kernel_ms_ratio": round(prof["avg_ns"] / 1e6 / kernel_ms, 4), "schedule": got}
+    if got != want:
+        out["note"] = f"profile schedule {got} differs from the timed one {want}: not cited"
+        return out
+    lv = prof["levels"]
+    t = kernel_ms * 1e-3
+    levels = {"l2": (lv["l2_request_bytes"], L2_PEAK_GBS), "fabric": (lv["fabric_bytes"], MALL_PEAK_GBS)}
+    fr = {k: b / t / 1e9 / peak for k, (b, peak) in levels.items()}
+    bound = max(fr, key=fr.get)
+    b, peak = levels[bound]
+    out.update({"bound": bound, "achieved": round(b / t / 1e9, 1), "peak": peak, "frac": round(fr[bound], 4),
+                "traffic": int(lv["fabric_bytes"]),
+                "levels": {k: {"bytes_per_launch": int(levels[k][0]), "GBps": round(levels[k][0] / t / 1e9, 1),
+                               "peak_GBps": levels[k][1], "frac": round(fr[k], 4)} for k in levels},
+                "l1_hit_fraction_of_algorithmic": round(max(0.0, 1.0 - lv["l2_request_bytes"] / alg_bytes_per_launch), 4),
+                "l2_hit_rate": prof.get("l2_hit_rate"),
+                "hbm_measured_GBps": round(lv["fabric_bytes"] / t / 1e9, 1),
+                "hbm_measured_frac": round(lv["fabric_bytes"] / t / 1e9 / HBM_PEAK_GBS, 4)})
+    return out
+
+
+def exploration_cost(tracer, gbvh, rb, exact, max_launches=200):
+    """What autotuning costs a caller without saved schedules: a fresh
+    bind, then blocking timed launches of one batch until its schedule locks; the
+    exploring launches' total against as many launches of the settled schedule.
+    The saved schedules are locked again afterwards."""
+    tracer.set_bvh(gbvh)
+    times, locked_at = [], None
+    for i in range(max_launches):
+        times.append(tracer.trace_batch(rb, exact_rcp=exact))
+        if tracer.last_info["autotune_locked"]:
+            locked_at = i + 1
+            break
+    settled = [tracer.trace_batch(rb, exact_rcp=exact) for _ in range(10)]
+    cand = tracer.last_info["autotune_candidate"]
+    bind(tracer, gbvh)
+    if locked_at is None:
+        return {"locked": False, "launches": max_launches}
+    s = float(np.median(settled))
+    return {"locked": True, "launches_to_lock": locked_at, "exploring_ms": round(sum(times), 3),
+            "settled_ms_each": round(s, 4), "overhead_ms": round(sum(times) - locked_at * s, 3),
+            "explored_candidate": cand}
 
 
 # cfg.autotune candidates (csrc/mrt_api.cpp tune_candidate)
 SCHEDULES = {0: "static rounds, 20 waves/CU", 1: "static rounds, 8 waves/CU", 2: "8 per-XCD queues",
              3: "global queue, refill at 48, 16 waves/CU", 4: "global queue, refill at 48, 12 waves/CU",
              5: "static rounds, 16 waves/CU", 6: "static rounds, 12 waves/CU",
-             7: "8 per-XCD queues, spec_slack 4",
-             8: "the best of 0-7 with spec_slack 4", 9: "the best of 0-7 with spec_slack 6"}
+             7: "8 per-XCD queues, spec_slack 4"}
 
 
-def run_workload(name, tracer, scenes, world, rank, steps, warmup, exact, want_cpu):
+def schedule_name(c):
+    """mrt_trace_info.autotune_candidate: 0-7 a schedule, 8/9 (| stage-1 schedule << 8) that
+    schedule with spec_slack 4/6, -1 the fixed rule (autotune off or several streams)."""
+    if c < 0:
+        return "fixed rule"
+    if (c & 0xff) >= 8:
+        return f"{SCHEDULES[c >> 8]}, spec_slack {4 if (c & 0xff) == 8 else 6}"
+    return SCHEDULES[c]
+
+
+def schedule_of(tracer, rb, exact):
+    """The schedule a batch's launches run on: one more blocking launch, outside the timed region."""
+    tracer.trace_batch(rb, exact_rcp=exact)
+    li = tracer.last_info
+    return {"autotune_candidate": li["autotune_candidate"], "autotune_locked": li["autotune_locked"],
+            "name": schedule_name(li["autotune_candidate"]), "num_queues": li["num_queues"],
+            "fetch_threshold": li["fetch_threshold"], "grid_waves": li["grid_waves"]}
+
+
+def run_workload(name, tracer, scenes, world, rank, steps, warmup, exact, want_cpu, explore=False, fast=False):
     scene_name = workload_spec(name)[0]
     e = scenes.get(scene_name)
     batches = Batches(name, e["scene"], e["gbvh"], tracer, rank)
@@ -514,14 +616,30 @@ def run_workload(name, tracer, scenes, world, rank, steps, warmup, exact, want_c
     alg_bytes = reduce_over_ranks(alg_bytes, world, "sum") / world   # per-GPU bytes (mean over ranks)
     value = counted * steps / wall / 1e6
     gather = gather_to_root(batches, world) if world > 1 else None
-    # the schedule the launches ran on (cfg.autotune settles during the warmup):
-    # one more blocking launch of the first batch, outside the timed region
-    tracer.trace_batch(batches.batches[0][0], exact_rcp=exact)
-    li = tracer.last_info
-    schedule = {"autotune_candidate": li["autotune_candidate"], "autotune_locked": li["autotune_locked"],
-                "name": SCHEDULES.get(li["autotune_candidate"], "fixed rule"), "num_queues": li["num_queues"],
-                "fetch_threshold": li["fetch_threshold"], "grid_waves": li["grid_waves"]}
+    # the schedule the launches ran on: saved for this BVH (locked at bind), or settled
+    # by the autotuner during the warmup
+    schedule = schedule_of(tracer, batches.batches[0][0], exact)
+    schedule["source"] = "saved (mrt/tuned_schedules.json)" if batches.locked_from_store else "autotuned in this run"
+    if LEARNED is not None:
+        LEARNED.update(e["gbvh"].fingerprint, tracer.schedules())
     g = e["gbvh"]
+    # the drop-in's default arithmetic (v_rcp_f32, the reference's rcp.approx analogue)
+    fast_block, fast_results = None, None
+    if fast:
+        fl = [tracer.launcher(rb, exact_rcp=False) for rb, _ in batches.batches]
+        fsteps = max(10, min(steps, 100))
+        fwall, fms, _ = time_steps(fl, fsteps, warmup, world)
+        fsched = schedule_of(tracer, batches.batches[0][0], False)
+        fast_results = []
+        for rb, _ in batches.batches:
+            tracer.trace_batch(rb, exact_rcp=False)
+            fast_results.append(rb.results_numpy())
+            tracer.trace_batch(rb, exact_rcp=exact)   # leave the exact results for the parity check
+        fast_block = {"value": round(batches.rays_counted * fsteps / fwall / 1e6, 2), "steps": fsteps,
+                      "kernel_ms_per_launch": round(fms, 4), "schedule": fsched,
+                      "roofline": roofline(name, alg_bytes / len(batches.batches), fms, g.total_bytes, fsched,
+                                           rcp="fast")}
+    explored = exploration_cost(tracer, g, batches.batches[0][0], exact) if explore else None
     out = {
         "workload": name,
         "value": round(value, 2),
@@ -537,19 +655,24 @@ def run_workload(name, tracer, scenes, world, rank, steps, warmup, exact, want_c
                    if gather else None),
         "scene_tris": e["scene"].num_triangles,
         "bvh": {"inner_nodes": g.nodes.numel() // 16, "woop_slots": g.woop.numel() // 4, "bytes": g.total_bytes,
-                "build_s": round(e["build_s"], 2), "from_cache": e["cached"],
+                "build_s": round(e["build_s"], 2), "from_cache": e["cached"], "bind_ms": round(batches.bind_ms, 2),
+                "stack_capacity": tracer.bind_info()["stack_capacity"],
                 **({"max_depth": e["stats"]["max_depth"], "sah": round(e["stats"]["sah_cost"], 2)}
                    if e["stats"] and not e["cached"] else {})},
         "per_ray": {"nodes": round(n_nodes / batches.rays_traced, 2), "tris": round(n_tris / batches.rays_traced, 2),
                     "leaves": round(n_leaves / batches.rays_traced, 2),
                     "bytes": round(alg_bytes / batches.rays_traced, 1)},
         "schedule": schedule,
-        "roofline": roofline(name, alg_bytes / len(batches.batches), launch_ms, g.total_bytes),
+        "autotune_exploration": explored,
+        "roofline": roofline(name, alg_bytes / len(batches.batches), launch_ms, g.total_bytes, schedule),
         "reference_mrays": REFERENCE_MRAYS.get(name),
+        "rcp_fast": fast_block,
     }
     if want_cpu:
         out["cpu_baseline"] = cpu_baseline(batches.batches, scenes.host_buffers(scene_name), batches.rays_counted,
-                                           host_threads(), name)
+                                           host_threads(), name, fast_results)
+        if fast_block is not None:
+            fast_block["parity"] = out["cpu_baseline"].pop("rcp_fast_parity")
     return out
 
 
@@ -568,7 +691,7 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact):
     from mrt.tracer import RayBuffer
     cfg = STRONG
     e = scenes.get(cfg["scene"])
-    tracer.set_bvh(e["gbvh"])
+    bind(tracer, e["gbvh"])
     cam, _ = e["scene"].camera()
     r = Renderer(tracer, e["scene"], max_batch=cfg["max_batch"], exact_rcp=True)
     r.set_params(RAY_DIFFUSE, cfg["spp"])
@@ -683,9 +806,22 @@ def main():
                     help="nccl (RCCL) for real runs; gloo only to rehearse N>1 ranks on one GPU")
     ap.add_argument("--lane-groups", type=int, default=0)
     ap.add_argument("--no-autotune", action="store_true", help="the fixed schedule rule instead of per-size autotuning")
+    ap.add_argument("--tune-db", default=None,
+                    help="saved schedules to lock (default: the package's mrt/tuned_schedules.json); '' = none, "
+                         "every batch size is autotuned during its warmup")
+    ap.add_argument("--save-schedules", default=None, help="write the schedules this run settled to this file "
+                                                             "(merged into the --tune-db store; tools/tune_db.sh)")
+    ap.add_argument("--no-explore", action="store_true", help="skip measuring the autotuner's exploration cost")
+    ap.add_argument("--no-fast", action="store_true", help="skip the fast-reciprocal (v_rcp_f32) measurement")
     args = ap.parse_args()
 
+    global STORE, LEARNED
+    from mrt.schedules import DEFAULT_PATH, ScheduleStore
     from mrt.tracer import Tracer
+    db = DEFAULT_PATH if args.tune_db is None else args.tune_db
+    STORE = ScheduleStore(db) if db else None
+    if args.save_schedules:
+        LEARNED = ScheduleStore(db) if db else ScheduleStore("")
 
     rank, world, local = dist_setup(args.gpus, args.dist_backend)
     tracer = Tracer(local)
@@ -708,14 +844,18 @@ def main():
     want_cpu = (rank == 0 and world == 1 and not args.no_cpu)
     scenes = SceneCache(world, rank, args.bvh_cache or None)
 
-    head = run_workload(args.workload, tracer, scenes, world, rank, args.steps, args.warmup, exact, want_cpu)
+    explore = want_cpu and not args.no_explore and not args.no_autotune
+    fast = want_cpu and exact and not args.no_fast
+    head = run_workload(args.workload, tracer, scenes, world, rank, args.steps, args.warmup, exact, want_cpu,
+                        explore, fast)
     log(f"[head] {args.workload}: {head['value']} Mrays/s")
     extras = []
     do_extra = args.extra if args.extra is not None else (world == 1)
     if do_extra:
         for name in EXTRA_N1:
             if name != args.workload:
-                r = run_workload(name, tracer, scenes, world, rank, args.steps, args.warmup, exact, want_cpu)
+                r = run_workload(name, tracer, scenes, world, rank, args.steps, args.warmup, exact, want_cpu,
+                                 explore, fast)
                 extras.append(r)
                 log(f"[extra] {name}: {r['value']} Mrays/s (reference {r['reference_mrays']}, "
                     f"cpu {r.get('cpu_baseline', {}).get('value')})")
@@ -764,13 +904,17 @@ def main():
             "strong_scaling": strong,
             "detail": {k: head[k] for k in ("kernel_ms_per_launch", "rays_traced", "mrays_traced_per_s", "bvh",
                                             "per_ray", "reference_mrays", "rays_counted_all_ranks", "gather",
-                                            "warmup_steps_run", "schedule")},
+                                            "warmup_steps_run", "schedule", "autotune_exploration")},
+            "rcp_fast": head.get("rcp_fast"),
             "extra_workloads": [{k: r.get(k) for k in ("workload", "value", "reference_mrays", "kernel_ms_per_launch",
                                                        "rays_counted", "rays_traced", "per_ray", "roofline", "bvh",
-                                                       "cpu_baseline", "schedule")}
+                                                       "cpu_baseline", "schedule", "rcp_fast", "autotune_exploration")}
                                 for r in extras],
         }
         print(json.dumps(line), flush=True)
+        if LEARNED is not None:
+            LEARNED.save(args.save_schedules)
+            log(f"[schedules] saved {sum(len(v) for v in LEARNED.table.values())} to {args.save_schedules}")
     if world > 1:
         import torch.distributed as dist
         dist.barrier()

@@ -9,6 +9,7 @@
 #include <climits>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -47,6 +48,13 @@ struct mrt_tracer {
     int wideBuiltFor = -1;   // the cfg.wide value the current array was built for
     int wideFormat = mrt::kNodeCompact2;   // the form wideNodes holds (kNodeWide4 / kNodeWide4Q)
     bool wideLeafCounts = false;           // its leaf refs carry triangle counts
+    // Stack entries (sentinel included) the wide traversal gets: the wide tree's
+    // worst case (wide_stack_bound) + 1, at least the reference's 64. A wide node
+    // pushes up to three children where the binary step pushes one, so a tree that
+    // fits the reference's stack in binary order could otherwise overflow in wide
+    // order; sized this way no ray of the bound tree can overflow it.
+    int wideStackCap = mrt::kStackCapacity;
+    double bindMs = 0.0;                   // wall time of the last bind / wide derivation (mrt_trace_info)
 
     // Launch scratch, one set per stream the handle has launched on: the stack
     // spill slab, the queue heads and the overflow counter are written by a
@@ -70,12 +78,13 @@ struct TuneState {
     // with the speculation slack at 4 and 6 (candidates kSchedules, kSchedules + 1).
     static constexpr int kSchedules = 8;
     static constexpr int kCandidates = kSchedules + 2;
-    static constexpr int kSamples = 4;   // timed launches per candidate (the minimum counts)
+    static constexpr int kSamples = 8;   // timed launches per candidate; the median ranks them
     int launches = 0;    // exploring launches so far (the first round of candidates runs untimed:
                          // the clocks and caches are still settling)
-    float best[kCandidates];
+    float times[kCandidates][kSamples];
     int samples[kCandidates] = {};
     int next = 0;        // candidate the next exploring launch uses
+    int rule = 0;        // the candidate equal to the fixed rule (effective_cfg) for this batch
     int stage1 = -1;     // the stage-1 winner, once every schedule has kSamples samples
     int locked = -1;     // the chosen candidate, once stage 2's have kSamples samples too
     void* stream = nullptr;          // the stream this batch size was first launched on
@@ -84,8 +93,12 @@ struct TuneState {
         hipEvent_t start = nullptr, stop = nullptr;
         int cand = -1;   // -1 = slot free
     } pending[16];   // launches in flight with a timing (back-to-back launches complete later)
-    TuneState() {
-        for (float& b : best) b = 1e30f;
+    float median(int c) const {
+        float v[kSamples];
+        const int n = std::min(samples[c], kSamples);
+        std::copy(times[c], times[c] + n, v);
+        std::sort(v, v + n);
+        return n ? (n % 2 ? v[n / 2] : 0.5f * (v[n / 2 - 1] + v[n / 2])) : 1e30f;
     }
 };
 
@@ -102,12 +115,22 @@ int api_fail(int code, const std::string& what) {
 const char* api_last_error() { return g_lastError.c_str(); }
 
 struct Workspace {
-    void* stream = nullptr;       // the hipStream_t this scratch belongs to
+    void* stream = nullptr;       // the hipStream_t this scratch was last used on
     unsigned* queues = nullptr;   // kMaxQueues * kQueueStrideWords words
-    int* status = nullptr;        // [0] = stack overflows since the last reset (sticky on the async path)
+    int* status = nullptr;        // [0] = stack overflows of asynchronous launches since the last reset
+                                  // (sticky); [kTimedSlot] = the current blocking launch's own count
     int* spill = nullptr;
     size_t spillInts = 0;
+    // Recorded after every launch that uses this scratch: waiting for it never
+    // touches the stream, which the caller may have destroyed since.
+    hipEvent_t done = nullptr;
+    bool launched = false;
+    uint64_t lastUse = 0;         // launch counter value of the last use (LRU reuse)
 };
+constexpr int kTimedSlot = 16;    // a separate 64-B line of Workspace::status
+// Scratch sets per handle: a trace on a new stream reuses the least recently used
+// set (after its last launch has completed) once this many exist.
+constexpr int kMaxWorkspaces = 8;
 }  // namespace mrt
 
 namespace {
@@ -266,11 +289,34 @@ int grid_blocks(mrt_tracer* t, const mrt_launch_cfg& cfg, const mrt::TraceVarian
     return perCU * t->numCUs;
 }
 
-// The scratch of `stream` (created on first use), grown to the grid's spill slab.
-int workspace_for(mrt_tracer* t, void* stream, int totalLanes, int ldsStack, mrt::Workspace** out) {
+// Waits for the last launch that used `w` (an event wait: the stream may be gone).
+int workspace_wait(mrt::Workspace* w) {
+    if (w->launched) MRT_HIP(hipEventSynchronize(w->done));
+    return MRT_OK;
+}
+
+// Every launch of this handle has completed (bind, set_config and destroy use it
+// instead of a device-wide synchronize, which would stall other users' streams).
+int wait_all_workspaces(mrt_tracer* t) {
+    for (mrt::Workspace* w : t->workspaces)
+        if (int rc = workspace_wait(w)) return rc;
+    return MRT_OK;
+}
+
+// The scratch of `stream`: its own set, else a new one, else (kMaxWorkspaces
+// reached) the least recently used set once its last launch has completed —
+// grown to the grid's spill slab.
+int workspace_for(mrt_tracer* t, void* stream, int totalLanes, int ldsStack, int stackCap, mrt::Workspace** out) {
+    static uint64_t useClock = 0;
     mrt::Workspace* w = nullptr;
     for (mrt::Workspace* x : t->workspaces)
         if (x->stream == stream) w = x;
+    if (!w && (int)t->workspaces.size() >= mrt::kMaxWorkspaces) {
+        for (mrt::Workspace* x : t->workspaces)
+            if (!w || x->lastUse < w->lastUse) w = x;
+        if (int rc = workspace_wait(w)) return rc;   // its previous stream's launch may still run
+        w->stream = stream;
+    }
     if (!w) {
         w = new mrt::Workspace();
         w->stream = stream;
@@ -278,11 +324,13 @@ int workspace_for(mrt_tracer* t, void* stream, int totalLanes, int ldsStack, mrt
         MRT_HIP(hipMalloc(&w->queues, mrt::kMaxQueues * mrt::kQueueStrideWords * sizeof(unsigned)));
         MRT_HIP(hipMalloc(&w->status, 64 * sizeof(int)));
         MRT_HIP(hipMemset(w->status, 0, 64 * sizeof(int)));
+        MRT_HIP(hipEventCreateWithFlags(&w->done, hipEventDisableTiming));
     }
-    const size_t need = (size_t)(mrt::kStackCapacity - ldsStack) * (size_t)totalLanes;
+    w->lastUse = ++useClock;
+    const size_t need = (size_t)(stackCap - ldsStack) * (size_t)totalLanes;
     if (need > w->spillInts) {
-        // A smaller slab may still be in use by this stream's previous launch.
-        MRT_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+        // A smaller slab may still be in use by this scratch's previous launch.
+        if (int rc = workspace_wait(w)) return rc;
         if (w->spill) MRT_HIP(hipFree(w->spill));
         w->spill = nullptr;
         w->spillInts = 0;
@@ -297,6 +345,9 @@ int workspace_for(mrt_tracer* t, void* stream, int totalLanes, int ldsStack, mrt
     return MRT_OK;
 }
 
+// Largest wide-traversal stack a tracer sizes its spill slab for (entries per lane).
+constexpr int kMaxWideStack = 1024;
+
 // (Re)derives the 4-wide nodes of the bound BVH when cfg.wide asks for them;
 // bind, unbind and set_config call it with the handle's mutex held. Synchronous
 // (bind-time work: the Compact2 nodes come to the host, collapse, go back).
@@ -304,12 +355,14 @@ int refresh_wide(mrt_tracer* t) {
     const int want = t->bound ? t->cfg.wide : 0;
     if (want == t->wideBuiltFor) return MRT_OK;
     DeviceGuard guard(t->device);
-    MRT_HIP(hipDeviceSynchronize());   // launches in flight may still read the old array
+    // launches in flight may still read the old array: wait for this handle's own
+    if (int rc = wait_all_workspaces(t)) return rc;
     if (t->wideNodes) MRT_HIP(hipFree(t->wideNodes));
     t->wideNodes = nullptr;
     t->wideBytes = 0;
     t->wideBuiltFor = -1;
     t->wideFormat = mrt::kNodeCompact2;
+    t->wideStackCap = mrt::kStackCapacity;
     if (want) {
         std::vector<int32_t> host((size_t)(t->nodeBytes / 4));
         MRT_HIP(hipMemcpy(host.data(), t->nodes, (size_t)t->nodeBytes, hipMemcpyDeviceToHost));
@@ -328,6 +381,13 @@ int refresh_wide(mrt_tracer* t) {
         if (want == 2 && mrt::build_wide4q(host.data(), t->nodeBytes / 64, &wide, wx, slots)) format = mrt::kNodeWide4Q;
         else wide = mrt::build_wide4(host.data(), t->nodeBytes / 64, wx, slots);
         t->wideLeafCounts = counts;
+        const int nodeWords = format == mrt::kNodeWide4 ? 32 : 16;
+        const int64_t need = mrt::wide_stack_bound(wide.data(), (int64_t)wide.size() / nodeWords, nodeWords);
+        if (need + 1 > kMaxWideStack) {   // a degenerate tree: keep the binary traversal and its reference capacity
+            t->wideBuiltFor = want;
+            return MRT_OK;
+        }
+        t->wideStackCap = std::max<int>(mrt::kStackCapacity, (int)need + 1);
         const int64_t bytes = (int64_t)wide.size() * 4;
         if (bytes > mrt::kMaxBufferBytes) return fail(MRT_ERR_TOO_LARGE, "4-wide node array above the 32-bit range");
         MRT_HIP(hipMalloc(&t->wideNodes, (size_t)bytes));
@@ -380,33 +440,38 @@ mrt_launch_cfg tune_candidate(const mrt_launch_cfg& base, int c, int stage1) {
     return x;
 }
 
+// A candidate replaces the incumbent (the fixed rule in stage 1, the stage-1 winner
+// in stage 2) only when its median is this much faster: candidates within a few
+// per cent of each other no longer settle differently from run to run.
+constexpr float kTuneMargin = 0.03f;
+
+int tune_pick(const TuneState* st, int incumbent, int first, int last) {
+    int best = incumbent;
+    for (int c = first; c < last; c++)
+        if (c != incumbent && st->median(c) < st->median(best)) best = c;
+    return st->median(best) < (1.0f - kTuneMargin) * st->median(incumbent) ? best : incumbent;
+}
+
 void tune_collect(TuneState* st) {
     for (auto& p : st->pending) {
         if (p.cand < 0 || hipEventQuery(p.stop) != hipSuccess) continue;
         float ms = 0.f;
-        if (hipEventElapsedTime(&ms, p.start, p.stop) == hipSuccess) {
-            st->best[p.cand] = std::min(st->best[p.cand], ms);
-            st->samples[p.cand]++;
-        }
+        if (hipEventElapsedTime(&ms, p.start, p.stop) == hipSuccess && st->samples[p.cand] < TuneState::kSamples)
+            st->times[p.cand][st->samples[p.cand]++] = ms;
         p.cand = -1;
     }
     if (st->locked >= 0) return;
     if (st->stage1 < 0) {
         for (int c = 0; c < TuneState::kSchedules; c++)
             if (st->samples[c] < TuneState::kSamples) return;
-        int best = 0;
-        for (int c = 1; c < TuneState::kSchedules; c++)
-            if (st->best[c] < st->best[best]) best = c;
-        st->stage1 = best;
+        st->stage1 = tune_pick(st, st->rule, 0, TuneState::kSchedules);
         st->next = TuneState::kSchedules;
         return;
     }
     for (int c = TuneState::kSchedules; c < TuneState::kCandidates; c++)
         if (st->samples[c] < TuneState::kSamples) return;
-    int best = st->stage1;
-    for (int c = TuneState::kSchedules; c < TuneState::kCandidates; c++)
-        if (st->best[c] < st->best[best]) best = c;
-    st->locked = best;
+    st->samples[st->stage1] = std::min(st->samples[st->stage1], TuneState::kSamples);
+    st->locked = tune_pick(st, st->stage1, TuneState::kSchedules, TuneState::kCandidates);
 }
 
 void tune_reset(mrt_tracer* t) {
@@ -458,11 +523,14 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
         } else if ((int)t->tunes.size() < kMaxTuned) {
             tune = new TuneState();
             tune->stream = stream;
+            // the candidate that equals the fixed rule for this batch (effective_cfg)
+            tune->rule = cfg.num_queues == 1 ? (cfg.waves_per_cu == kBigQueueWaves ? 3 : 4) : 0;
             t->tunes[key] = tune;
         }
         // A batch size launched on several streams keeps the fixed rule: its launches
         // overlap, and a schedule's time alone no longer ranks the pipeline (the
         // bench's two-stream hairball buffer: 5.2 ms on the rule, 6.2 tuned alone).
+        if (tune && !tune->stream) tune->stream = stream;   // an imported schedule: first used here
         if (tune && tune->stream != stream) tune->multiStream = true;
         if (tune && tune->multiStream) tune = nullptr;
     }
@@ -489,13 +557,14 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     }
     const int blocks = grid_blocks(t, cfg, v, numRays, &perCU);
     const int totalLanes = blocks * mrt::kBlockThreads;
+    const bool wide = v.nodes != mrt::kNodeCompact2;
+    const int stackCap = wide ? t->wideStackCap : mrt::kStackCapacity;
     mrt::Workspace* ws = nullptr;
-    if (int rc = workspace_for(t, stream, totalLanes, v.ldsStack, &ws)) return rc;
+    if (int rc = workspace_for(t, stream, totalLanes, v.ldsStack, stackCap, &ws)) return rc;
 
     mrt::TraceArgs a{};
     a.rays = static_cast<const float4*>(rays);
     a.results = static_cast<int2*>(results);
-    const bool wide = v.nodes != mrt::kNodeCompact2;
     a.nodes = static_cast<const float4*>(wide ? t->wideNodes : t->nodes);
     a.woop = static_cast<const float4*>(t->woop);
     a.triIndex = t->triIndex;
@@ -509,28 +578,33 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     a.wideLeafCounts = wide && t->wideLeafCounts;
     a.laneGroupsLog2 = __builtin_ctz((unsigned)cfg.lane_groups);
     a.totalLanes = totalLanes;
+    a.stackCap = stackCap;
     a.queues = ws->queues;
     a.spill = ws->spill;
-    a.status = ws->status;
+    // The blocking call counts this launch's overflows in a slot of its own; the
+    // asynchronous one adds to the sticky counter (mrt_tracer_stack_overflows).
+    a.status = info ? ws->status + mrt::kTimedSlot : ws->status;
     a.stats = reinterpret_cast<int4*>(stats);
 
     hipStream_t s = static_cast<hipStream_t>(stream);
     // Queue heads restart at zero for every launch; strided mode has none.
     if (a.numQueues > 0)
         MRT_HIP(hipMemsetAsync(ws->queues, 0, mrt::kMaxQueues * mrt::kQueueStrideWords * sizeof(unsigned), s));
-    // The blocking call reports this launch's overflows alone; the asynchronous
-    // one leaves the counter sticky (mrt_tracer_stack_overflows reads it).
-    if (info) MRT_HIP(hipMemsetAsync(ws->status, 0, sizeof(int), s));
+    if (info) MRT_HIP(hipMemsetAsync(ws->status + mrt::kTimedSlot, 0, sizeof(int), s));
     if (info) MRT_HIP(hipEventRecord(t->evStart, s));
     if (slot) MRT_HIP(hipEventRecord(slot->start, s));
     MRT_HIP(mrt::launch_trace(v, a, blocks, s));
+    MRT_HIP(hipEventRecord(ws->done, s));
+    ws->launched = true;
     if (slot) {
         MRT_HIP(hipEventRecord(slot->stop, s));
         slot->cand = cand;
     }
     if (info) {
-        info->autotune_candidate = cand;
+        // stage-2 candidates (another speculation slack) carry their stage-1 schedule in bits 8+
+        info->autotune_candidate = cand >= TuneState::kSchedules ? cand | (tune->stage1 << 8) : cand;
         info->autotune_locked = tune && tune->locked >= 0 ? 1 : 0;
+        info->stack_capacity = stackCap;
         MRT_HIP(hipEventRecord(t->evStop, s));
         MRT_HIP(hipEventSynchronize(t->evStop));
         MRT_HIP(hipEventElapsedTime(&info->kernel_ms, t->evStart, t->evStop));
@@ -542,7 +616,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
         info->num_queues = a.numQueues;
         info->fetch_threshold = a.fetchThreshold;
         int overflow = 0;
-        MRT_HIP(hipMemcpy(&overflow, ws->status, sizeof(int), hipMemcpyDeviceToHost));
+        MRT_HIP(hipMemcpy(&overflow, ws->status + mrt::kTimedSlot, sizeof(int), hipMemcpyDeviceToHost));
         info->stack_overflows = overflow;
         if (overflow)
             return fail(MRT_ERR_STACK_OVERFLOW, std::to_string(overflow) +
@@ -645,8 +719,9 @@ int mrt_tracer_destroy(mrt_tracer* t) {
     {
         DeviceGuard guard(t->device);
         if (t->wideNodes) (void)hipFree(t->wideNodes);
+        (void)wait_all_workspaces(t);   // event waits: the streams may already be destroyed
         for (mrt::Workspace* w : t->workspaces) {
-            if (w->stream) (void)hipStreamSynchronize(static_cast<hipStream_t>(w->stream));
+            if (w->done) (void)hipEventDestroy(w->done);
             if (w->queues) (void)hipFree(w->queues);
             if (w->status) (void)hipFree(w->status);
             if (w->spill) (void)hipFree(w->spill);
@@ -680,7 +755,10 @@ int mrt_tracer_bind(mrt_tracer* t, const void* nodes, int64_t nodeBytes, const v
     t->wideBuiltFor = -1;   // a new BVH: its wide nodes are derived now (if configured)
     DeviceGuard guard(t->device);
     tune_reset(t);          // and its schedules are tuned again
-    return refresh_wide(t);
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = refresh_wide(t);
+    t->bindMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
 }
 
 int mrt_tracer_unbind(mrt_tracer* t) {
@@ -709,12 +787,65 @@ int mrt_tracer_set_config(mrt_tracer* t, const mrt_launch_cfg* cfg) {
     t->cfg = c;
     DeviceGuard guard(t->device);
     tune_reset(t);
-    return refresh_wide(t);
+    const auto t0 = std::chrono::steady_clock::now();
+    const int built = t->wideBuiltFor;
+    const int rc = refresh_wide(t);
+    if (t->wideBuiltFor != built)
+        t->bindMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
 }
 
 int mrt_tracer_get_config(const mrt_tracer* t, mrt_launch_cfg* cfg) {
     if (!t || !cfg) return fail(MRT_ERR_INVALID_ARG, "null argument");
     *cfg = t->cfg;
+    return MRT_OK;
+}
+
+int mrt_tracer_bind_info(const mrt_tracer* t, mrt_bind_info* info) {
+    if (!t || !info) return fail(MRT_ERR_INVALID_ARG, "null argument");
+    info->bind_ms = t->bindMs;
+    info->wide_bytes = t->wideNodes ? t->wideBytes : 0;
+    info->wide_format = t->wideNodes ? t->wideFormat : mrt::kNodeCompact2;
+    info->stack_capacity = t->wideNodes ? t->wideStackCap : mrt::kStackCapacity;
+    return MRT_OK;
+}
+
+// candidate field: the locked candidate | the stage-1 winner << 8 (stage-2 candidates
+// are the stage-1 schedule with another speculation slack)
+int mrt_tracer_tune_export(const mrt_tracer* t, mrt_tuned_schedule* out, int32_t capacity, int32_t* count) {
+    if (!t || !count || (capacity > 0 && !out)) return fail(MRT_ERR_INVALID_ARG, "null argument");
+    std::lock_guard<std::mutex> lock(const_cast<mrt_tracer*>(t)->mu);
+    int n = 0;
+    for (const auto& kv : t->tunes) {
+        if (kv.second->locked < 0) continue;
+        if (n < capacity)
+            out[n] = mrt_tuned_schedule{kv.first.first, kv.first.second,
+                                        kv.second->locked | (std::max(0, kv.second->stage1) << 8), MRT_TUNE_VERSION};
+        n++;
+    }
+    *count = n;
+    return MRT_OK;
+}
+
+int mrt_tracer_tune_import(mrt_tracer* t, const mrt_tuned_schedule* in, int32_t count) {
+    if (!t || (count > 0 && !in) || count < 0) return fail(MRT_ERR_INVALID_ARG, "null argument");
+    for (int i = 0; i < count; i++) {
+        const int locked = in[i].candidate & 0xff, stage1 = in[i].candidate >> 8;
+        if (in[i].version != MRT_TUNE_VERSION || in[i].num_rays <= 0 || locked >= TuneState::kCandidates ||
+            stage1 < 0 || stage1 >= TuneState::kSchedules)
+            return fail(MRT_ERR_INVALID_ARG, "tuned schedule from another library version or out of range");
+    }
+    std::lock_guard<std::mutex> lock(t->mu);
+    for (int i = 0; i < count; i++) {
+        const auto key = std::make_pair((int)in[i].num_rays, (int)in[i].variant);
+        auto it = t->tunes.find(key);
+        if (it == t->tunes.end()) {
+            if ((int)t->tunes.size() >= kMaxTuned) return fail(MRT_ERR_TOO_LARGE, "more tuned batch sizes than kMaxTuned");
+            it = t->tunes.emplace(key, new TuneState()).first;
+        }
+        it->second->stage1 = in[i].candidate >> 8;
+        it->second->locked = in[i].candidate & 0xff;
+    }
     return MRT_OK;
 }
 
@@ -736,7 +867,7 @@ int mrt_tracer_stack_overflows(mrt_tracer* t, int64_t* count, int32_t reset) {
     int64_t total = 0;
     for (mrt::Workspace* w : t->workspaces) {
         int n = 0;
-        MRT_HIP(hipStreamSynchronize(static_cast<hipStream_t>(w->stream)));
+        if (int rc = workspace_wait(w)) return rc;
         MRT_HIP(hipMemcpy(&n, w->status, sizeof(int), hipMemcpyDeviceToHost));
         total += n;
         if (reset) MRT_HIP(hipMemset(w->status, 0, sizeof(int)));

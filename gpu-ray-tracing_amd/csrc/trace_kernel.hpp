@@ -42,8 +42,9 @@ struct TraceArgs {
     int wideLeafCounts;        // the wide leaf refs carry triangle counts (wide_bvh.cpp)
     int laneGroupsLog2;        // strided mode: a wave's lanes take rays from 2^k spread-out sub-ranges
     int totalLanes;            // grid lanes (stride of the spill slab)
+    int stackCap;              // stack entries incl. the sentinel (kStackCapacity, or the wide tree's bound)
     unsigned* queues;          // numQueues heads, kQueueStrideWords apart, zeroed per launch
-    int* spill;                // (kStackCapacity - S) * totalLanes ints
+    int* spill;                // (stackCap - S) * totalLanes ints
     int* status;               // [0] = stack overflow count (lanes that pushed past kStackCapacity)
     int4* stats;               // per-ray {nodes, tris, leaves, 0} (STATS variants)
 };
@@ -71,6 +72,12 @@ constexpr int kWideLeafAddrBits = 27;
 bool leaf_counts_fit(int64_t woopSlots);
 std::vector<uint32_t> build_wide4(const int32_t* nodes, int64_t numNodes, const int32_t* woopX = nullptr,
                                   int64_t woopSlots = 0);
+// The most stack entries (sentinel excluded) a traversal of a 4-wide node array
+// can hold: the maximum over nodes of the pushes of all their ancestors plus
+// their own (each node pushes all but one of its children when every child is
+// hit, and any child may be the one visited first). nodeWords: 32 (exact form)
+// or 16 (quantized).
+int64_t wide_stack_bound(const uint32_t* wide, int64_t numWide, int nodeWords);
 // The quantized 4-wide form: 16 uint32 (64 B) per wide node. False (and no
 // output) when some child box has no finite quantization (non-finite planes).
 bool build_wide4q(const int32_t* nodes, int64_t numNodes, std::vector<uint32_t>* out, const int32_t* woopX = nullptr,

@@ -39,7 +39,18 @@ class LaunchCfg(C.Structure):
 class TraceInfo(C.Structure):
     _fields_ = [("kernel_ms", f32), ("grid_waves", i32), ("block_threads", i32),
                 ("lds_stack_entries", i32), ("wide", i32), ("num_queues", i32), ("fetch_threshold", i32), ("stack_overflows", i32), ("node_bytes", i32),
-                ("autotune_candidate", i32), ("autotune_locked", i32)]
+                ("autotune_candidate", i32), ("autotune_locked", i32), ("stack_capacity", i32)]
+
+
+class BindInfo(C.Structure):
+    _fields_ = [("bind_ms", C.c_double), ("wide_bytes", i64), ("wide_format", i32), ("stack_capacity", i32)]
+
+
+class TunedSchedule(C.Structure):
+    _fields_ = [("num_rays", i32), ("variant", i32), ("candidate", i32), ("version", i32)]
+
+
+MRT_TUNE_VERSION = 3
 
 
 class HostCamera(C.Structure):
@@ -65,6 +76,9 @@ TRACE_SYMBOLS = [
     ("mrt_tracer_unbind", i32, [vp]),
     ("mrt_tracer_set_config", i32, [vp, C.POINTER(LaunchCfg)]),
     ("mrt_tracer_get_config", i32, [vp, C.POINTER(LaunchCfg)]),
+    ("mrt_tracer_bind_info", i32, [vp, C.POINTER(BindInfo)]),
+    ("mrt_tracer_tune_export", i32, [vp, C.POINTER(TunedSchedule), i32, C.POINTER(i32)]),
+    ("mrt_tracer_tune_import", i32, [vp, C.POINTER(TunedSchedule), i32]),
     ("mrt_tracer_trace", i32, [vp, vp, vp, i32, u32, vp, vp]),
     ("mrt_tracer_trace_timed", i32, [vp, vp, vp, i32, u32, vp, vp, C.POINTER(TraceInfo)]),
     ("mrt_tracer_stack_overflows", i32, [vp, C.POINTER(i64), i32]),

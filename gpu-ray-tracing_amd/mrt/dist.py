@@ -14,6 +14,12 @@ import torch
 import torch.distributed as dist
 
 
+def _on_device(t: torch.Tensor) -> bool:
+    """RCCL moves HBM-resident tensors only (tests/test_dist_mock.py replaces this
+    check to dry-run the nccl branches on the CPU)."""
+    return t.device.type == "cuda"
+
+
 def shard_range(n: int, world: int, rank: int) -> tuple[int, int]:
     """Contiguous shard [lo, hi) of n rays for `rank` (sizes differ by at most one)."""
     base, extra = divmod(n, world)
@@ -63,8 +69,21 @@ def replicate_buffers(bufs, src: int = 0, device=None):
     they stay in HBM (the BVH crosses xGMI once and is bound in place, GpuBvh
     accepts them without a copy); with gloo they are CPU tensors."""
     rank = dist.get_rank()
+    nccl = dist.get_backend() == "nccl"
     dev = device if device is not None else (torch.device("cuda", torch.cuda.current_device())
-                                             if dist.get_backend() == "nccl" else torch.device("cpu"))
+                                             if nccl else torch.device("cpu"))
+    dev = torch.device(dev)
+    if nccl and not _on_device(torch.empty(0, device=dev)):
+        raise ValueError("replicate_buffers: RCCL (nccl) broadcasts device tensors; got device " + str(dev))
+    if rank == src:
+        if bufs is None or len(bufs) == 0:
+            raise ValueError("replicate_buffers: the source rank must pass the buffers")
+        for b in bufs:
+            dt = b.dtype if isinstance(b, torch.Tensor) else np.asarray(b).dtype
+            if dt not in (torch.int32, np.int32, np.dtype(np.int32)):
+                raise TypeError(f"replicate_buffers: int32 buffers expected (Compact2 words), got {dt}")
+            if (b.dim() if isinstance(b, torch.Tensor) else np.ndim(b)) != 1:
+                raise ValueError("replicate_buffers: flat 1-D buffers expected")
     count = len(bufs) if rank == src else 0
     meta = torch.tensor([count], dtype=torch.int64, device=dev)
     dist.broadcast(meta, src)
@@ -79,6 +98,8 @@ def replicate_buffers(bufs, src: int = 0, device=None):
                  else torch.from_numpy(np.ascontiguousarray(b, np.int32)).to(dev))
         else:
             t = torch.empty(int(sizes[i]), dtype=torch.int32, device=dev)
+        if t.numel() != int(sizes[i]) or t.device != dev:
+            raise RuntimeError("replicate_buffers: buffer shape/device changed before the broadcast")
         dist.broadcast(t, src)
         out.append(t)
     return out
@@ -111,6 +132,9 @@ def trace_shard(tracer, rays, world: int, rank: int, max_rays: int = 1 << 21, ex
         return lo, hi
     from .tracer import RayBuffer
     local = RayBuffer(local_rays(rays.rays, shard_spans(rays.size, world, rank, block)), rays.need_closest_hit)
+    if stream is not None:
+        # the local buffer was built on the current stream: the launches on `stream` wait for it
+        stream.wait_stream(torch.cuda.current_stream())
     for a, b in shard_launches(0, local.size, max_rays):
         tracer.trace_async(local.view(a, b), exact_rcp=exact_rcp, stream=stream)
     return local
@@ -124,6 +148,15 @@ def gather_results(local: torch.Tensor, n_total: int, dst: int = 0, block: int =
     block-cyclic shard arrives as one message and is scattered into place with
     one index_copy_. Returns the full array on `dst`, None elsewhere."""
     world, rank = dist.get_world_size(), dist.get_rank()
+    if local.dtype != torch.int32 or local.dim() != 2 or local.shape[1] < 2:
+        raise TypeError(f"gather_results: RayResult rows (int32 [k, >=2]) expected, got {local.dtype} "
+                        f"{tuple(local.shape)}")
+    if dist.get_backend() == "nccl" and not _on_device(local):
+        raise ValueError("gather_results: RCCL (nccl) moves device tensors; got a " + local.device.type + " tensor")
+    mine = sum(b - a for a, b in shard_spans(n_total, world, rank, block))
+    if local.shape[0] != mine:
+        raise ValueError(f"gather_results: rank {rank} holds {local.shape[0]} results, its shard of {n_total} "
+                         f"rays has {mine}")
     payload = local[:, :2].contiguous()
     if rank != dst:
         if payload.shape[0] > 0:

@@ -129,6 +129,27 @@ class Tracer:
         c = _lib.LaunchCfg(**cur)
         _lib.check(self.lib.mrt_tracer_set_config(self._h, C.byref(c)))
 
+    def bind_info(self) -> dict:
+        """What the last bind derived: wall ms, wide-node bytes/format, stack capacity."""
+        b = _lib.BindInfo()
+        _lib.check(self.lib.mrt_tracer_bind_info(self._h, C.byref(b)))
+        return {k: getattr(b, k) for k, _ in b._fields_}
+
+    def schedules(self) -> list:
+        """The autotuner's settled schedules [(num_rays, variant, candidate, version)]."""
+        n = C.c_int32()
+        _lib.check(self.lib.mrt_tracer_tune_export(self._h, None, 0, C.byref(n)))
+        arr = (_lib.TunedSchedule * max(1, n.value))()
+        _lib.check(self.lib.mrt_tracer_tune_export(self._h, arr, n.value, C.byref(n)))
+        return [(e.num_rays, e.variant, e.candidate, e.version) for e in arr[:n.value]]
+
+    def load_schedules(self, entries) -> None:
+        """Lock schedules saved by schedules() from an earlier run on the same BVH
+        (call after set_bvh: binding forgets them)."""
+        entries = list(entries)
+        arr = (_lib.TunedSchedule * max(1, len(entries)))(*[_lib.TunedSchedule(*e) for e in entries])
+        _lib.check(self.lib.mrt_tracer_tune_import(self._h, arr, len(entries)))
+
     # -- CudaTracer API --------------------------------------------------------
     def set_bvh(self, bvh: GpuBvh) -> None:
         """setBVH + bind_CudaBVHTexture (CudaTracer.cc:142-146); re-binding is allowed."""

@@ -117,7 +117,30 @@ typedef struct mrt_trace_info {
     int32_t node_bytes;        /* bytes per node the launch read: 64 (Compact2 or quantized 4-wide), 128 */
     int32_t autotune_candidate; /* cfg.autotune: the schedule candidate this launch used (0..9), else -1 */
     int32_t autotune_locked;   /* 1 once the batch size's schedule is chosen                      */
+    int32_t stack_capacity;    /* stack entries (sentinel included) the launch had: 64 = the reference's
+                                  for the binary order; the wide orders get the bound tree's worst case
+                                  (never less than 64), so no ray of a tree overflows there          */
 } mrt_trace_info;
+
+/* What the last bind derived (mrt_tracer_bind_info). */
+typedef struct mrt_bind_info {
+    double  bind_ms;           /* wall time of the last bind / set_config's wide-node derivation      */
+    int64_t wide_bytes;        /* bytes of the derived 4-wide node array (0 = the Compact2 nodes)      */
+    int32_t wide_format;       /* 0 = Compact2, 1 = exact 4-wide (128 B), 2 = quantized 4-wide (64 B)  */
+    int32_t stack_capacity;    /* stack entries the wide traversal gets (see mrt_trace_info)          */
+} mrt_bind_info;
+
+/* One settled launch schedule of the autotuner (cfg.autotune): the candidate a batch
+ * size and kernel variant chose. Opaque apart from num_rays; valid for the library
+ * version MRT_TUNE_VERSION and the BVH it was tuned on (the caller keys a saved
+ * table by the BVH, e.g. next to its .dat cache). */
+typedef struct mrt_tuned_schedule {
+    int32_t num_rays;
+    int32_t variant;
+    int32_t candidate;
+    int32_t version;           /* MRT_TUNE_VERSION when exported; others are refused on import */
+} mrt_tuned_schedule;
+enum { MRT_TUNE_VERSION = 3 };
 
 /* ---- handle API -------------------------------------------------------- */
 int  mrt_tracer_create(int device, mrt_tracer** out);
@@ -134,6 +157,14 @@ int  mrt_tracer_unbind(mrt_tracer* t);
 
 int  mrt_tracer_set_config(mrt_tracer* t, const mrt_launch_cfg* cfg);
 int  mrt_tracer_get_config(const mrt_tracer* t, mrt_launch_cfg* cfg);
+int  mrt_tracer_bind_info(const mrt_tracer* t, mrt_bind_info* info);
+
+/* The autotuner's settled schedules (up to capacity; *count = how many exist), and
+ * the reverse: schedules saved from an earlier run of the same BVH are locked at
+ * once (no exploring launches, the same schedule every run). Import after bind
+ * (bind and set_config forget every schedule). */
+int  mrt_tracer_tune_export(const mrt_tracer* t, mrt_tuned_schedule* out, int32_t capacity, int32_t* count);
+int  mrt_tracer_tune_import(mrt_tracer* t, const mrt_tuned_schedule* in, int32_t count);
 
 /* Stream-ordered trace of numRays (<= 2^30) rays (device pointers). stream is a
  * hipStream_t (NULL = the null stream). stats may be NULL unless

@@ -27,6 +27,8 @@ def lib():
         L.oracle_trace.argtypes = [vp, vp, i64, C.c_int, vp, i64, vp, i64, vp, vp, C.c_int]
         L.oracle_woop_hit.restype = C.c_int
         L.oracle_woop_hit.argtypes = [vp, vp, i64, i64, C.c_float, C.POINTER(C.c_float)]
+        L.oracle_woop_hit_rcp.restype = C.c_int
+        L.oracle_woop_hit_rcp.argtypes = [vp, vp, i64, i64, C.c_float, C.c_int, C.POINTER(C.c_float)]
         L.oracle_brute_force.restype = None
         L.oracle_brute_force.argtypes = [vp, vp, i64, C.c_int, vp, i64, vp]
         L.oracle_tri_colors.restype = None
@@ -63,6 +65,83 @@ def woop_hit(ray, woop, slot, tmax):
     t = C.c_float()
     hit = lib().oracle_woop_hit(_p(ray), _p(woop), woop.nbytes, int(slot), float(tmax), C.byref(t))
     return bool(hit), float(t.value)
+
+
+def woop_hit_rcp(ray, woop, slot, tmax, rcp_ulps):
+    """The Woop test with 1/Dz moved by rcp_ulps ulps (oracle_woop_hit_rcp)."""
+    ray = np.ascontiguousarray(ray, np.float32).reshape(8)
+    woop = np.ascontiguousarray(woop).view(np.int32)
+    t = C.c_float()
+    hit = lib().oracle_woop_hit_rcp(_p(ray), _p(woop), woop.nbytes, int(slot), float(tmax), int(rcp_ulps),
+                                    C.byref(t))
+    return bool(hit), float(t.value)
+
+
+def _ulps(a, b):
+    ia, ib = (int(np.float32(x).view(np.int32)) for x in (a, b))
+    ia = -(ia & 0x7FFFFFFF) if ia < 0 else ia
+    ib = -(ib & 0x7FFFFFFF) if ib < 0 else ib
+    return abs(ia - ib)
+
+
+def classify_fast_rcp(rays, gpu, want, woop, tri_index, limit=20000):
+    """SURVEY.md §8(a) Note 3: closest-hit results of the fast-reciprocal mode
+    (v_rcp_f32, the analogue of the reference's rcp.approx) against the oracle's
+    correctly rounded ones. A ray agrees when its id is equal and t within 2 ulp.
+    A mismatch is
+      * "tie":  both triangles are valid hits of the ray under the exact Woop test
+                and their t lie within 4 ulp of each other (traversal order decides);
+      * "edge": the oracle's triangle fails, or the GPU's passes, the Woop test once
+                1/Dz moves by one ulp (v_rcp_f32's error bound): the outcome is
+                decided by the reciprocal's rounding (a grazing ray on an edge);
+      * "other": anything else (a real error; expected 0).
+    Returns counts and up to 20 example rays per class."""
+    rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)
+    woop = np.ascontiguousarray(woop).view(np.int32)
+    tri = np.ascontiguousarray(tri_index, np.int32)
+    woop4 = woop.reshape(-1, 4)
+    live = woop4[:, 0] != np.int32(-2147483648)
+    g_id, w_id = gpu[:, 0], want[:, 0]
+    g_t, w_t = gpu[:, 1].view(np.float32), want[:, 1].view(np.float32)
+    # ulp distance of t, vectorised
+    def ord_(x):
+        i = x.view(np.int32).astype(np.int64)
+        return np.where(i < 0, -(i & 0x7FFFFFFF), i)
+    dt = np.abs(ord_(g_t) - ord_(w_t))
+    bad = np.nonzero((g_id != w_id) | (dt > 2))[0]
+    out = {"rays": int(len(rays)), "mismatch": int(len(bad)), "tie": 0, "edge": 0, "other": 0,
+           "examples": {"tie": [], "edge": [], "other": []}}
+    slots_of = {}
+
+    def slots(tid):
+        if tid not in slots_of:
+            slots_of[tid] = np.nonzero((tri == tid) & live)[0]
+        return slots_of[tid]
+    for i in bad[:limit]:
+        r = rays[i]
+        tmax = float(r[7])
+        cls = "other"
+        if g_id[i] != -1 and w_id[i] != -1:
+            exact_g = [t for s in slots(int(g_id[i])) for h, t in [woop_hit(r, woop, s, tmax)] if h]
+            if exact_g and min(_ulps(t, w_t[i]) for t in exact_g) <= 4 and _ulps(g_t[i], w_t[i]) <= 4:
+                cls = "tie"
+        if cls == "other":
+            flips = False
+            for tid, wanted in ((int(w_id[i]), True), (int(g_id[i]), False)):
+                if tid == -1:
+                    continue
+                for s in slots(tid):
+                    res = [woop_hit_rcp(r, woop, s, tmax, k)[0] for k in (-1, 0, 1)]
+                    if len(set(res)) > 1:
+                        flips = True
+            # the oracle's hit missed by the GPU, or a GPU hit the oracle did not take, decided by 1/Dz rounding
+            if flips:
+                cls = "edge"
+        out[cls] += 1
+        if len(out["examples"][cls]) < 20:
+            out["examples"][cls].append([int(i), int(g_id[i]), float(g_t[i]), int(w_id[i]), float(w_t[i])])
+    out["unclassified"] = int(max(0, len(bad) - limit))
+    return out
 
 
 def brute_force(rays, woop, tri_index, any_hit=False):

@@ -1,9 +1,19 @@
-"""Condense a tools/profile_round.sh output directory into profiles/<tag>_*:
-the rocprofv3 kernel-stats CSV as-is, and a JSON with the per-launch PMC
-values of the timed trace kernel (FETCH_SIZE / WRITE_SIZE in KB as rocprofv3
-reports them, gfx950 read correction per MI355X_MICROARCH.md §HBM)."""
+"""Condense a tools/profile_round.sh output directory into profiles/<tag>_*: the
+rocprofv3 kernel-stats CSV as-is, and a JSON with the per-launch PMC values of the
+timed trace kernel and the bytes each cache level served (bench.py roofline()):
+  l2_request_bytes = TCP_TCC_READ_REQ x 128     (lines the L1s fetched from L2)
+  fabric_bytes     = TCC_EA0_RDREQ x 128 (32-B requests x 32) + WRITE_SIZE
+                     (L2 misses served by the Infinity Cache or HBM, and writes)
+128 B per request: gfx950's line, calibrated by tools/ubench_levels.hip
+(profiles/round3_counter_calibration.md). The schedule the profiled launches ran
+(from the bench's own JSON line in the kernel-trace pass) is recorded, so the bench
+cites the profile only for the schedule it times.
+
+Only launches of the timed kernel with the timed grid count: the mean kernel
+duration is taken over those dispatches in the kernel trace."""
 import collections
 import csv
+import glob
 import json
 import os
 import shutil
@@ -15,32 +25,46 @@ dst = os.path.join(repo, "profiles")
 os.makedirs(dst, exist_ok=True)
 shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
 
-# the timed kernel = the trace_kernel instantiation with the most calls
+
+def bench_line(log):
+    for line in open(log):
+        if line.startswith("{"):
+            return json.loads(line)
+    return None
+
+
+line = bench_line(os.path.join(src, "bench_kt.log"))
+sched = line["detail"]["schedule"] if line else None
+grid = sched["grid_waves"] * 64 if sched else None
+
+# the timed kernel = the trace_kernel instantiation with the most calls; its dispatches at the timed grid
 stats = list(csv.DictReader(open(os.path.join(src, "kt", "run_kernel_stats.csv"))))
 timed = max((r for r in stats if "trace_kernel" in r["Name"]), key=lambda r: int(r["Calls"]))
-out = {"kernel": timed["Name"], "calls": int(timed["Calls"]), "avg_ns": float(timed["AverageNs"]),
-       "min_ns": float(timed["MinNs"]), "max_ns": float(timed["MaxNs"]), "pmc": {}}
+durs = []
+for f in glob.glob(os.path.join(src, "kt", "run_kernel_trace.csv")):
+    for r in csv.DictReader(open(f)):
+        if r["Kernel_Name"] == timed["Name"] and (grid is None or int(r["Grid_Size"]) == grid):
+            durs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+out = {"kernel": timed["Name"], "calls": int(timed["Calls"]), "avg_ns_all_calls": float(timed["AverageNs"]),
+       "timed_grid_calls": len(durs), "avg_ns": (sum(durs) / len(durs)) if durs else float(timed["AverageNs"]),
+       "min_ns": float(timed["MinNs"]), "max_ns": float(timed["MaxNs"]), "schedule": sched,
+       "bench_value": line["value"] if line else None, "pmc": {}}
 for p in sorted(d for d in os.listdir(src) if d.startswith("pmc")):
     rows = list(csv.DictReader(open(os.path.join(src, p, "run_counter_collection.csv"))))
     vals = collections.defaultdict(list)
-    grid = {}
     for r in rows:
-        if r["Kernel_Name"] == timed["Name"]:
+        if r["Kernel_Name"] == timed["Name"] and (grid is None or int(r["Grid_Size"]) == grid):
             vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-            grid = {"grid_size": int(r["Grid_Size"]), "rocprof_VGPR_Count_field": int(r["VGPR_Count"]), "lds": int(r["LDS_Block_Size"])}
+            out.update({"grid_size": int(r["Grid_Size"]), "lds": int(r["LDS_Block_Size"])})
     for k, v in vals.items():
         out["pmc"][k] = {"per_launch_mean": sum(v) / len(v), "launches": len(v)}
-    out.update(grid)
-pm = out["pmc"]
-if "FETCH_SIZE" in pm and "WRITE_SIZE" in pm:
-    fetch = pm["FETCH_SIZE"]["per_launch_mean"] * 1024
-    write = pm["WRITE_SIZE"]["per_launch_mean"] * 1024
-    out["hbm_bytes_per_launch"] = {"fetch_raw": fetch, "fetch_corrected_x2": 2 * fetch, "write": write,
-                                   "total_corrected": 2 * fetch + write,
-                                   "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM (gfx950 reports 1/2 of "
-                                           "wide reads); our 16-B-per-lane gathers are not a calibrated width"}
+pm = {k: v["per_launch_mean"] for k, v in out["pmc"].items()}
+need = ("TCP_TCC_READ_REQ_sum", "TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "WRITE_SIZE")
+if all(k in pm for k in need):
+    rd = (pm["TCC_EA0_RDREQ_sum"] - pm["TCC_EA0_RDREQ_32B_sum"]) * 128 + pm["TCC_EA0_RDREQ_32B_sum"] * 32
+    out["levels"] = {"l2_request_bytes": pm["TCP_TCC_READ_REQ_sum"] * 128, "fabric_read_bytes": rd,
+                     "write_bytes": pm["WRITE_SIZE"] * 1024, "fabric_bytes": rd + pm["WRITE_SIZE"] * 1024}
 if "TCC_HIT_sum" in pm and "TCC_MISS_sum" in pm:
-    h, m = pm["TCC_HIT_sum"]["per_launch_mean"], pm["TCC_MISS_sum"]["per_launch_mean"]
-    out["l2_hit_rate"] = h / (h + m)
+    out["l2_hit_rate"] = pm["TCC_HIT_sum"] / (pm["TCC_HIT_sum"] + pm["TCC_MISS_sum"])
 json.dump(out, open(os.path.join(dst, f"{tag}_pmc_summary.json"), "w"), indent=1)
-print(json.dumps(out, indent=1))
+print(json.dumps({k: out.get(k) for k in ("kernel", "avg_ns", "timed_grid_calls", "schedule", "levels", "l2_hit_rate")}))
