@@ -563,10 +563,17 @@ void gen_random(Scene& sc, int64_t count, uint64_t seed) {   // uniformly scatte
     for (int64_t i = 0; i < count; i++) {
         const double cx = rng.range(-1, 1), cy = rng.range(-1, 1), cz = rng.range(-1, 1);
         const double s = rng.range(0.02, 0.15);
-        const int a = m.vert(cx + s * rng.range(-1, 1), cy + s * rng.range(-1, 1), cz + s * rng.range(-1, 1));
-        const int b = m.vert(cx + s * rng.range(-1, 1), cy + s * rng.range(-1, 1), cz + s * rng.range(-1, 1));
-        const int c = m.vert(cx + s * rng.range(-1, 1), cy + s * rng.range(-1, 1), cz + s * rng.range(-1, 1));
-        m.tri(a, b, c);
+        // One offset per coordinate, drawn z, y, x: the order GCC evaluated the three
+        // draws in when they were vert()'s arguments (unspecified in C++; the golden
+        // fixtures were built that way, tests/golden/make_golden.py). Sequenced
+        // explicitly so every compiler builds the same scene (found by the clang
+        // sanitizer build, tools/sanitize_host.sh).
+        int v[3];
+        for (int& k : v) {
+            const double oz = rng.range(-1, 1), oy = rng.range(-1, 1), ox = rng.range(-1, 1);
+            k = m.vert(cx + s * ox, cy + s * oy, cz + s * oz);
+        }
+        m.tri(v[0], v[1], v[2]);
     }
     sc.camera = look_at(Vec3f(0.f, 0.2f, 3.2f), Vec3f(0.f, 0.f, 0.f), Vec3f(0.f, 1.f, 0.f), 50.f, 0.01f, 100.f);
     sc.aoRadius = 0.5f;

@@ -171,6 +171,12 @@ constexpr int kDefaultSpecSlack = 2;
 // Launch schedules are tuned per batch size (autotune_*, below): equal or faster on
 // every workload once settled (+9...+16 % on bunny/dragon primary batches).
 constexpr int kDefaultAutotune = 1;
+// The cooperative tail (trace_kernel.hip cooperative_tail): at most this many live
+// lanes of a wave that cannot refill finish four lanes per ray.
+#ifndef MRT_DEFAULT_TAIL_LANES
+#define MRT_DEFAULT_TAIL_LANES 16
+#endif
+constexpr int kDefaultTailLanes = MRT_DEFAULT_TAIL_LANES;
 
 mrt_launch_cfg default_cfg() {
     mrt_launch_cfg c;
@@ -183,6 +189,7 @@ mrt_launch_cfg default_cfg() {
     c.spec_slack = kDefaultSpecSlack;
     c.static_rounds = 1;
     c.autotune = kDefaultAutotune;
+    c.tail_lanes = kDefaultTailLanes;
     return c;
 }
 
@@ -192,7 +199,8 @@ bool valid_cfg(const mrt_launch_cfg& c) {
            (c.lds_stack == 8 || c.lds_stack == 16 || c.lds_stack == 32) &&
            c.lane_groups >= 1 && c.lane_groups <= 64 && (c.lane_groups & (c.lane_groups - 1)) == 0 &&
            (c.wide >= 0 && c.wide <= 2) && c.spec_slack >= 0 && c.spec_slack <= 63 &&
-           c.static_rounds >= 1 && c.static_rounds <= 64 && (c.autotune == 0 || c.autotune == 1);
+           c.static_rounds >= 1 && c.static_rounds <= 64 && (c.autotune == 0 || c.autotune == 1) &&
+           c.tail_lanes >= 0 && c.tail_lanes <= 16;
 }
 
 mrt::TraceVariant variant_for(const mrt_tracer* t, uint32_t flags) {
@@ -579,6 +587,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     a.laneGroupsLog2 = __builtin_ctz((unsigned)cfg.lane_groups);
     a.totalLanes = totalLanes;
     a.stackCap = stackCap;
+    a.tailLanes = cfg.tail_lanes;
     a.queues = ws->queues;
     a.spill = ws->spill;
     // The blocking call counts this launch's overflows in a slot of its own; the
@@ -782,6 +791,7 @@ int mrt_tracer_set_config(mrt_tracer* t, const mrt_launch_cfg* cfg) {
     if (c.spec_slack < 0) c.spec_slack = d.spec_slack;
     if (c.static_rounds == 0) c.static_rounds = d.static_rounds;
     if (c.autotune < 0) c.autotune = d.autotune;
+    if (c.tail_lanes < 0) c.tail_lanes = d.tail_lanes;
     if (!valid_cfg(c)) return fail(MRT_ERR_INVALID_ARG, "launch config out of range");
     std::lock_guard<std::mutex> lock(t->mu);
     t->cfg = c;

@@ -101,6 +101,10 @@ typedef struct mrt_launch_cfg {
                                   blocking, after one untimed round of them, and keep the fastest (a batch size launched on more than one stream keeps the
                                   fixed rule); reset by bind and set_config (default 1). 0 = the fixed
                                   rule only; -1 = library default */
+    int32_t tail_lanes;        /* exact 4-wide speculative traversal: a wave that cannot refill (its strided
+                                  round, or its queue drained) and is down to at most this many tracing
+                                  lanes finishes those rays four lanes per ray, one node or up to four
+                                  triangles per ray per memory round trip (0..16; 0 = off; -1 = default) */
 } mrt_launch_cfg;
 
 /* Per-launch statistics reported back to the host (optional). */

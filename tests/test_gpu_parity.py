@@ -209,7 +209,12 @@ def test_exact_reciprocal_is_correctly_rounded_for_every_float(tracer):
                                  dict(lds_stack=32, waves_per_cu=4, fetch_threshold=48),
                                  dict(num_queues=1, fetch_threshold=48, waves_per_cu=16), dict(lane_groups=2),
                                  dict(lane_groups=8), dict(lane_groups=64, waves_per_cu=4), dict(spec_slack=0),
-                                 dict(spec_slack=63), dict(spec_slack=7, num_queues=2, fetch_threshold=40)],
+                                 dict(spec_slack=63), dict(spec_slack=7, num_queues=2, fetch_threshold=40),
+                                 dict(tail_lanes=0), dict(tail_lanes=1), dict(tail_lanes=4),
+                                 dict(tail_lanes=16, waves_per_cu=4), dict(tail_lanes=16, lds_stack=8),
+                                 dict(tail_lanes=16, num_queues=1, fetch_threshold=48, waves_per_cu=4),
+                                 dict(tail_lanes=12, num_queues=8, waves_per_cu=4, static_rounds=2),
+                                 dict(tail_lanes=16, num_queues=-1, fetch_threshold=16)],
                          ids=lambda c: ",".join(f"{k}={v}" for k, v in c.items()))
 def test_launch_configs_do_not_change_results(tracer, cfg):
     bufs, rays, any_hit, want, st = scene_setup("conference", 256, 192, "diffuse")
@@ -313,6 +318,53 @@ def test_stack_overflow_is_reported(tracer, depth, overflow):
     tracer.set_config(**saved)
 
 
+@pytest.mark.parametrize("rays_n", [1, 5, 16, 17, 40])
+@pytest.mark.parametrize("depth", [10, 40, 63, 70])
+def test_cooperative_tail_on_deep_stacks(tracer, depth, rays_n):
+    """The cooperative tail (cfg.tail_lanes) takes a wave's last <= 16 rays four lanes
+    per ray; their stacks stay in the home lanes' LDS and spill columns. A batch of a
+    few comb rays enters it at once and pushes through the spill slab: the hand
+    answer for every ray, closest and any hit."""
+    from mrt.tracer import GpuBvh, RayBuffer
+    bufs, ray, expect = kat.scene_comb(depth)
+    saved = tracer.config()
+    try:
+        tracer.set_config(wide=1, tail_lanes=16)
+        tracer.set_bvh(GpuBvh(bufs))
+        for closest in (True, False):
+            rb = RayBuffer(np.stack([ray] * rays_n), need_closest_hit=closest)
+            rb.results.fill_(0x5A5A5A5A)
+            tracer.trace_batch(rb, exact_rcp=True)
+            res = rb.results_numpy()
+            assert tracer.last_info["stack_overflows"] == 0
+            assert (res[:, 2:] == 0x5A5A5A5A).all()
+            if closest:
+                assert (res[:, 0] == expect[0]).all() and (res[:, 1] == kat.f2i(expect[1])).all()
+            else:
+                assert (res[:, 0] >= 0).all()
+    finally:
+        tracer.set_config(**saved)
+
+
+@pytest.mark.parametrize("wl", WORKLOADS, ids=lambda w: "-".join(map(str, w)))
+@pytest.mark.parametrize("tail", [0, 16])
+def test_tail_lanes_keep_results(tracer, wl, tail):
+    """Closest hits bit-identical to the oracle with the cooperative tail off and at
+    its widest (the tail tests the same leaves; within a leaf the first of equal t
+    wins, as in the sequential loop); any hit: genuine hits, same hit/miss."""
+    bufs, rays, any_hit, want, _ = scene_setup(*wl)
+    saved = tracer.config()
+    try:
+        tracer.set_config(tail_lanes=tail, waves_per_cu=4)
+        res, _ = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=True)
+    finally:
+        tracer.set_config(**saved)
+    if any_hit:
+        assert_valid_hits(rays, res, want, bufs)
+    else:
+        assert np.array_equal(res[:, :2], want[:, :2])
+
+
 def test_timed_trace_keeps_async_overflow_count(tracer):
     """a blocking trace counts its own overflows in a slot of its own; the
     sticky counter of earlier asynchronous launches on the stream is not reset by it."""
@@ -326,10 +378,15 @@ def test_timed_trace_keeps_async_overflow_count(tracer):
     _lib.check(tracer.lib.mrt_tracer_stack_overflows(tracer._h, C.byref(n), 1))
     rb = RayBuffer(np.stack([ray] * 64), need_closest_hit=True)
     tracer.trace_async(rb, exact_rcp=True, speculative=False)        # overflows, sticky
+    _lib.check(tracer.lib.mrt_tracer_stack_overflows(tracer._h, C.byref(n), 1))
+    one = n.value                                                    # one launch's pushes past capacity
+    assert one == 64 * (70 - 63)
+    tracer.trace_async(rb, exact_rcp=True, speculative=False)
     with pytest.raises(_lib.MrtError, match="stack overflow"):
         tracer.trace_batch(rb, exact_rcp=True, speculative=False)    # its own count
+    assert tracer.last_info["stack_overflows"] == one
     _lib.check(tracer.lib.mrt_tracer_stack_overflows(tracer._h, C.byref(n), 1))
-    assert n.value == 64   # the async launch's 64 lanes, not reset by the blocking one, not added to
+    assert n.value == one   # the async launch's count: not reset by the blocking one, not added to
     tracer.set_config(**saved)
 
 
