@@ -75,9 +75,11 @@ struct mrt_tracer {
 // Launch-schedule autotuning state of one (batch size, kernel variant).
 struct TuneState {
     // Stage 1: kSchedules ray-distribution schedules; stage 2: the stage-1 winner
-    // with the speculation slack at 4 and 6 (candidates kSchedules, kSchedules + 1).
+    // with the speculation slack at 4 and 6, and without the cooperative tail
+    // (candidates kSchedules .. kSchedules + 2).
     static constexpr int kSchedules = 8;
-    static constexpr int kCandidates = kSchedules + 2;
+    static constexpr int kStage2 = 3;
+    static constexpr int kCandidates = kSchedules + kStage2;
     static constexpr int kSamples = 8;   // timed launches per candidate; the median ranks them
     int launches = 0;    // exploring launches so far (the first round of candidates runs untimed:
                          // the clocks and caches are still settling)
@@ -423,9 +425,12 @@ constexpr int kMaxTuned = 64;   // batch sizes tuned per handle; others use the 
 mrt_launch_cfg tune_candidate(const mrt_launch_cfg& base, int c, int stage1) {
     if (c >= TuneState::kSchedules) {
         // stage 2: the stage-1 winner, the wave turning to its leaves once <= 4 (6) lanes
-        // still search (only when the caller left spec_slack at its default)
+        // still search, or without the cooperative tail (only for knobs the caller left
+        // at their defaults)
         mrt_launch_cfg x = tune_candidate(base, stage1, stage1);
-        if (base.spec_slack == kDefaultSpecSlack) x.spec_slack = c == TuneState::kSchedules ? 4 : 6;
+        const int k = c - TuneState::kSchedules;
+        if (k < 2 && base.spec_slack == kDefaultSpecSlack) x.spec_slack = k == 0 ? 4 : 6;
+        if (k == 2 && base.tail_lanes == kDefaultTailLanes) x.tail_lanes = 0;
         return x;
     }
     mrt_launch_cfg x = base;
@@ -549,7 +554,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
         } else {
             cand = tune->next;
             tune->next = tune->stage1 < 0 ? (tune->next + 1) % TuneState::kSchedules
-                                          : TuneState::kSchedules + (tune->next + 1 - TuneState::kSchedules) % 2;
+                                          : TuneState::kSchedules + (tune->next + 1 - TuneState::kSchedules) % TuneState::kStage2;
             if (tune->launches++ >= TuneState::kSchedules)
                 for (auto& p : tune->pending)
                     if (p.cand < 0) {

@@ -96,11 +96,13 @@ typedef struct mrt_launch_cfg {
                                   of each batch size (per kernel variant, up to 64 sizes) time eight ray-
                                   distribution schedules (static rounds at 20, 16, 12 or 8 waves/CU, per-XCD
                                   queues with spec_slack 2 or 4, the global queue at 16 or 12 waves/CU), then
-                                  the winner with spec_slack 4 and 6 (when left at its default), four
-                                  times each without
-                                  blocking, after one untimed round of them, and keep the fastest (a batch size launched on more than one stream keeps the
-                                  fixed rule); reset by bind and set_config (default 1). 0 = the fixed
-                                  rule only; -1 = library default */
+                                  the winner with spec_slack 4 and 6 and without the cooperative tail (each
+                                  knob only when left at its default), eight times each without blocking,
+                                  after one untimed round of them; the median ranks them and a candidate
+                                  replaces the fixed rule (stage 1) or the stage-1 winner (stage 2) only
+                                  when 3 % faster. A batch size launched on more than one stream keeps the
+                                  fixed rule; reset by bind and set_config (default 1; mrt_tracer_tune_export /
+                                  _import save and restore the choices). 0 = the fixed rule only; -1 = default */
     int32_t tail_lanes;        /* exact 4-wide speculative traversal: a wave that cannot refill (its strided
                                   round, or its queue drained) and is down to at most this many tracing
                                   lanes finishes those rays four lanes per ray, one node or up to four
@@ -144,7 +146,7 @@ typedef struct mrt_tuned_schedule {
     int32_t candidate;
     int32_t version;           /* MRT_TUNE_VERSION when exported; others are refused on import */
 } mrt_tuned_schedule;
-enum { MRT_TUNE_VERSION = 3 };
+enum { MRT_TUNE_VERSION = 4 };
 
 /* ---- handle API -------------------------------------------------------- */
 int  mrt_tracer_create(int device, mrt_tracer** out);

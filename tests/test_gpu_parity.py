@@ -382,9 +382,8 @@ def test_timed_trace_keeps_async_overflow_count(tracer):
     one = n.value                                                    # one launch's pushes past capacity
     assert one == 64 * (70 - 63)
     tracer.trace_async(rb, exact_rcp=True, speculative=False)
-    with pytest.raises(_lib.MrtError, match="stack overflow"):
+    with pytest.raises(_lib.MrtError, match=f"{one} stack pushes"):
         tracer.trace_batch(rb, exact_rcp=True, speculative=False)    # its own count
-    assert tracer.last_info["stack_overflows"] == one
     _lib.check(tracer.lib.mrt_tracer_stack_overflows(tracer._h, C.byref(n), 1))
     assert n.value == one   # the async launch's count: not reset by the blocking one, not added to
     tracer.set_config(**saved)
