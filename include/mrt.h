@@ -107,6 +107,10 @@ typedef struct mrt_launch_cfg {
                                   round, or its queue drained) and is down to at most this many tracing
                                   lanes finishes those rays four lanes per ray, one node or up to four
                                   triangles per ray per memory round trip (0..16; 0 = off; -1 = default) */
+    int32_t steal;             /* queue modes (num_queues >= 2): 1 = a wave whose XCD's queue is dry takes rays
+                                  from the back of the other queues (one 64-bit atomic per wave refill; the
+                                  owners keep taking from the front, so each XCD stays on its own Morton
+                                  range until the end); 0 (default) = no stealing */
 } mrt_launch_cfg;
 
 /* Per-launch statistics reported back to the host (optional). */
