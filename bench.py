@@ -400,9 +400,10 @@ def warm(launches, warmup, min_seconds=0.3):
 
 def time_steps(launches, steps, warmup, world):
     """Warmup, then exactly `steps` steps bracketed by barrier + synchronize; wall
-    time of the K steps (a multi-stream step is joined: see joined()). Then a probe pass on the same stream: every launch
-    bracketed by its own HIP event pair, the mean of which is the kernel's
-    average launch duration (without inter-launch gaps)."""
+    time of the K steps (a multi-stream step is joined: see joined()). Then a probe
+    pass: the average launch duration, from one HIP event pair on the launch stream
+    around back-to-back launches (several streams: every launch bracketed by its own
+    pair, one at a time)."""
     import torch
     warmed = warm(launches, warmup)
     torch.cuda.synchronize()
@@ -417,9 +418,21 @@ def time_steps(launches, steps, warmup, world):
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     probe = max(3, min(steps, 50))
+    one_stream = all(go.stream == launches[0].stream for go in launches)
+    if one_stream:
+        # one event pair around `probe` back-to-back steps on the launch stream: an event
+        # recorded between launches fences the caches (a system-scope release), so
+        # bracketing every launch would time each one from cold caches
+        a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a_.record(launches[0].stream)
+        for _ in range(probe):
+            for go in launches:
+                go()
+        b_.record(launches[0].stream)
+        torch.cuda.synchronize()
+        return wall, a_.elapsed_time(b_) / (probe * len(launches)), warmed
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(probe * len(launches))]
-    one_stream = all(go.stream == launches[0].stream for go in launches)
     k = 0
     for _ in range(probe):
         for go in launches:
@@ -427,8 +440,7 @@ def time_steps(launches, steps, warmup, world):
             go()
             ev[k][1].record(go.stream)
             k += 1
-            if not one_stream:
-                torch.cuda.synchronize()   # one launch at a time: its own duration, not an overlap
+            torch.cuda.synchronize()   # one launch at a time: its own duration, not an overlap
     torch.cuda.synchronize()
     per_launch = [a.elapsed_time(b) for a, b in ev]
     return wall, float(np.mean(per_launch)), warmed

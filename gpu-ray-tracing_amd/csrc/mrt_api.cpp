@@ -65,7 +65,7 @@ struct mrt_tracer {
 
     // Occupancy per kernel variant (index variant_key(), below 256), queried once
     // (hipOccupancy* is a host round-trip that would otherwise sit on every launch).
-    int occ[256] = {};
+    int occ[512] = {};
 
     // cfg.autotune: per (batch size, variant) the ray-distribution schedule the
     // measured launches chose (mrt_api.cpp autotune_*), reset on bind/set_config.
@@ -130,6 +130,18 @@ struct Workspace {
     uint64_t lastUse = 0;         // launch counter value of the last use (LRU reuse)
 };
 constexpr int kTimedSlot = 16;    // a separate 64-B line of Workspace::status
+// The per-launch completion event only tells the host that the launch has finished
+// (workspace reuse, destroy, overflow reads): no system-scope fence, which would
+// write back and invalidate the caches between back-to-back launches.
+#ifndef MRT_DONE_EVENT_FLAGS
+#define MRT_DONE_EVENT_FLAGS (hipEventDisableTiming | hipEventDisableSystemFence)
+#endif
+constexpr unsigned kDoneEventFlags = MRT_DONE_EVENT_FLAGS;
+// Events that only time launches (the autotuner's, the blocking call's start).
+#ifndef MRT_TIMING_EVENT_FLAGS
+#define MRT_TIMING_EVENT_FLAGS hipEventDisableSystemFence
+#endif
+constexpr unsigned kTimingEventFlags = MRT_TIMING_EVENT_FLAGS;
 // Scratch sets per handle: a trace on a new stream reuses the least recently used
 // set (after its last launch has completed) once this many exist.
 constexpr int kMaxWorkspaces = 8;
@@ -206,6 +218,11 @@ bool valid_cfg(const mrt_launch_cfg& c) {
            c.tail_lanes >= 0 && c.tail_lanes <= 16 && (c.steal == 0 || c.steal == 1);
 }
 
+// The cooperative tail runs in the exact 4-wide kernels whose leaf refs carry counts.
+bool with_tail(const mrt_tracer* t, const mrt::TraceVariant& v, const mrt_launch_cfg& c) {
+    return c.tail_lanes > 0 && v.nodes == mrt::kNodeWide4 && t->wideLeafCounts;
+}
+
 mrt::TraceVariant variant_for(const mrt_tracer* t, uint32_t flags) {
     mrt::TraceVariant v;
     v.anyHit = (flags & MRT_TRACE_ANY_HIT) != 0;
@@ -216,6 +233,7 @@ mrt::TraceVariant variant_for(const mrt_tracer* t, uint32_t flags) {
     // The per-lane (lockstep-off) order is the reference's binary order: it keeps
     // the Compact2 nodes, and with them the oracle's exact per-ray counters.
     v.nodes = (t->cfg.wide != 0 && t->wideNodes != nullptr && v.speculative) ? t->wideFormat : mrt::kNodeCompact2;
+    v.tail = with_tail(t, v, t->cfg);
     return v;
 }
 
@@ -239,10 +257,10 @@ constexpr int kAutoMinWaves = 8;
 // workgroup is resident at once.
 int variant_key(const mrt::TraceVariant& v) {
     const int lds = v.ldsStack == 8 ? 0 : v.ldsStack == 16 ? 1 : 2;
-    static_assert((15 | (2 << 4) | (mrt::kNodeWide4Q << 6)) < (int)(sizeof(mrt_tracer::occ) / sizeof(int)),
+    static_assert((15 | (2 << 4) | (mrt::kNodeWide4Q << 6) | (1 << 8)) < (int)(sizeof(mrt_tracer::occ) / sizeof(int)),
                   "every variant_key indexes mrt_tracer::occ");
     return (v.anyHit ? 1 : 0) | (v.speculative ? 2 : 0) | (v.exactRcp ? 4 : 0) | (v.stats ? 8 : 0) | (lds << 4) |
-           (v.nodes << 6);   // < 256 = the size of mrt_tracer::occ
+           (v.nodes << 6) | (v.tail ? 256 : 0);   // < 512 = the size of mrt_tracer::occ
 }
 
 // The launch configuration a trace uses: the tracer's, except that with every
@@ -335,7 +353,7 @@ int workspace_for(mrt_tracer* t, void* stream, int totalLanes, int ldsStack, int
         MRT_HIP(hipMalloc(&w->queues, mrt::kMaxQueues * mrt::kQueueStrideWords * sizeof(unsigned)));
         MRT_HIP(hipMalloc(&w->status, 64 * sizeof(int)));
         MRT_HIP(hipMemset(w->status, 0, 64 * sizeof(int)));
-        MRT_HIP(hipEventCreateWithFlags(&w->done, hipEventDisableTiming));
+        MRT_HIP(hipEventCreateWithFlags(&w->done, mrt::kDoneEventFlags));
     }
     w->lastUse = ++useClock;
     const size_t need = (size_t)(stackCap - ldsStack) * (size_t)totalLanes;
@@ -349,8 +367,11 @@ int workspace_for(mrt_tracer* t, void* stream, int totalLanes, int ldsStack, int
         w->spillInts = need;
     }
     if (!t->evStart) {
-        MRT_HIP(hipEventCreate(&t->evStart));
-        MRT_HIP(hipEventCreate(&t->evStop));
+        // the blocking call's timing pair: no system-scope fence around the kernel (it would
+        // flush the caches and be timed with it); the stop event releases to device scope,
+        // so the overflow count read after it is current
+        MRT_HIP(hipEventCreateWithFlags(&t->evStart, mrt::kTimingEventFlags));
+        MRT_HIP(hipEventCreateWithFlags(&t->evStop, hipEventReleaseToDevice));
     }
     *out = w;
     return MRT_OK;
@@ -520,7 +541,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     if (numRays > kMaxRaysPerLaunch) return fail(MRT_ERR_TOO_LARGE, "more than 2^30 rays in one launch: split the batch");
 
     DeviceGuard guard(t->device);
-    const mrt::TraceVariant v = variant_for(t, flags);
+    mrt::TraceVariant v = variant_for(t, flags);   // its key (the tracer's tail setting) keys the tuning
     int perCU = 0;
     mrt_launch_cfg cfg = effective_cfg(t, numRays);
     // autotuning: the schedule candidate this launch uses, and its timing slot
@@ -563,12 +584,13 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
                         break;
                     }
             if (slot && !slot->start) {
-                MRT_HIP(hipEventCreate(&slot->start));
-                MRT_HIP(hipEventCreate(&slot->stop));
+                MRT_HIP(hipEventCreateWithFlags(&slot->start, mrt::kTimingEventFlags));
+                MRT_HIP(hipEventCreateWithFlags(&slot->stop, mrt::kTimingEventFlags));
             }
         }
         cfg = tune_candidate(cfg, cand, tune->stage1);
     }
+    v.tail = with_tail(t, v, cfg);   // a tuned candidate may run without the tail
     const int blocks = grid_blocks(t, cfg, v, numRays, &perCU);
     const int totalLanes = blocks * mrt::kBlockThreads;
     const bool wide = v.nodes != mrt::kNodeCompact2;
@@ -610,8 +632,10 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     if (info) MRT_HIP(hipEventRecord(t->evStart, s));
     if (slot) MRT_HIP(hipEventRecord(slot->start, s));
     MRT_HIP(mrt::launch_trace(v, a, blocks, s));
+#ifndef MRT_NO_DONE_EVENT
     MRT_HIP(hipEventRecord(ws->done, s));
     ws->launched = true;
+#endif
     if (slot) {
         MRT_HIP(hipEventRecord(slot->stop, s));
         slot->cand = cand;

@@ -64,6 +64,7 @@ struct TraceVariant {
     bool stats;
     int ldsStack;       // 8, 16 or 32 LDS entries per lane
     int nodes = 0;      // kNodeCompact2, or a 4-wide form derived from it (speculative mode only)
+    bool tail = false;  // kNodeWide4 with leaf counts: the instantiation with the cooperative tail
 };
 
 // The 4-wide node array derived from a Compact2 node array (numNodes inner nodes,

@@ -46,18 +46,17 @@ def main():
                 launches = [tracer.launcher(rb, exact_rcp=not args.fast_rcp) for rb, _ in batches.batches]
                 for go in launches * 3:   # settle
                     go()
-                ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                      for _ in range(args.launches * len(launches))]
-                k = 0
+                # one event pair around back-to-back launches (an event between launches
+                # fences the caches)
+                a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a_.record()
                 for _ in range(args.launches):
                     for go in launches:
-                        ev[k][0].record()
                         go()
-                        ev[k][1].record()
-                        k += 1
+                b_.record()
                 torch.cuda.synchronize()
                 if r:   # round 0 is a warmup
-                    times[i].append(float(np.median([a.elapsed_time(b) for a, b in ev])) * len(launches))
+                    times[i].append(a_.elapsed_time(b_) / args.launches)
         tracer.set_config(**base)
         line = [f"{wl:28s}"]
         for i, c in enumerate(cfgs):
