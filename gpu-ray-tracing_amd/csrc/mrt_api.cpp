@@ -75,8 +75,8 @@ struct mrt_tracer {
 // Launch-schedule autotuning state of one (batch size, kernel variant).
 struct TuneState {
     // Stage 1: kSchedules ray-distribution schedules; stage 2: the stage-1 winner
-    // with the speculation slack at 4 and 6, and without the cooperative tail
-    // (candidates kSchedules .. kSchedules + 2).
+    // with the speculation slack at 4 and 6, and with the cooperative tail (without it
+    // if the tracer's default has it) (candidates kSchedules .. kSchedules + 2).
     static constexpr int kSchedules = 8;
     static constexpr int kStage2 = 3;
     static constexpr int kCandidates = kSchedules + kStage2;
@@ -123,20 +123,22 @@ struct Workspace {
                                   // (sticky); [kTimedSlot] = the current blocking launch's own count
     int* spill = nullptr;
     size_t spillInts = 0;
-    // Recorded after every launch that uses this scratch: waiting for it never
-    // touches the stream, which the caller may have destroyed since.
+    // -DMRT_DONE_EVENT: recorded after every launch that uses this scratch, so waiting
+    // for it never touches the stream (see workspace_wait)
     hipEvent_t done = nullptr;
-    bool launched = false;
+    bool launched = false;        // a launch may still be using this scratch
     uint64_t lastUse = 0;         // launch counter value of the last use (LRU reuse)
 };
 constexpr int kTimedSlot = 16;    // a separate 64-B line of Workspace::status
 // The per-launch completion event only tells the host that the launch has finished
 // (workspace reuse, destroy, overflow reads): no system-scope fence, which would
 // write back and invalidate the caches between back-to-back launches.
+#ifdef MRT_DONE_EVENT
 #ifndef MRT_DONE_EVENT_FLAGS
 #define MRT_DONE_EVENT_FLAGS (hipEventDisableTiming | hipEventDisableSystemFence)
 #endif
 constexpr unsigned kDoneEventFlags = MRT_DONE_EVENT_FLAGS;
+#endif
 // Events that only time launches (the autotuner's, the blocking call's start).
 #ifndef MRT_TIMING_EVENT_FLAGS
 #define MRT_TIMING_EVENT_FLAGS hipEventDisableSystemFence
@@ -188,8 +190,10 @@ constexpr int kDefaultAutotune = 1;
 // The cooperative tail (trace_kernel.hip cooperative_tail): at most this many live
 // lanes of a wave that cannot refill finish four lanes per ray.
 #ifndef MRT_DEFAULT_TAIL_LANES
-#define MRT_DEFAULT_TAIL_LANES 16
+#define MRT_DEFAULT_TAIL_LANES 0
 #endif
+// What the autotuner's stage 2 tries when tail_lanes is left at its default (0).
+constexpr int kTunedTailLanes = 16;
 constexpr int kDefaultTailLanes = MRT_DEFAULT_TAIL_LANES;
 
 mrt_launch_cfg default_cfg() {
@@ -318,14 +322,25 @@ int grid_blocks(mrt_tracer* t, const mrt_launch_cfg& cfg, const mrt::TraceVarian
     return perCU * t->numCUs;
 }
 
-// Waits for the last launch that used `w` (an event wait: the stream may be gone).
+// Waits for the last launch that used `w` without touching the stream it ran on (the
+// caller may have destroyed it): a device-wide synchronize. A completion event recorded
+// after every launch (-DMRT_DONE_EVENT) would let the wait cover this handle's launches
+// only, but an event between back-to-back launches costs each of them 1-3 % (measured:
+// conference AO 0.0352 -> 0.0361 ms, bunny 640x480 0.0945 -> 0.0959 ms,
+// profiles/round3_tuning.md); the waits are rare (bind, set_config, destroy, overflow
+// reads, a ninth stream).
 int workspace_wait(mrt::Workspace* w) {
-    if (w->launched) MRT_HIP(hipEventSynchronize(w->done));
+    if (!w->launched) return MRT_OK;
+#ifdef MRT_DONE_EVENT
+    MRT_HIP(hipEventSynchronize(w->done));
+#else
+    MRT_HIP(hipDeviceSynchronize());
+    w->launched = false;
+#endif
     return MRT_OK;
 }
 
-// Every launch of this handle has completed (bind, set_config and destroy use it
-// instead of a device-wide synchronize, which would stall other users' streams).
+// Every launch of this handle has completed (bind, set_config and destroy).
 int wait_all_workspaces(mrt_tracer* t) {
     for (mrt::Workspace* w : t->workspaces)
         if (int rc = workspace_wait(w)) return rc;
@@ -353,7 +368,9 @@ int workspace_for(mrt_tracer* t, void* stream, int totalLanes, int ldsStack, int
         MRT_HIP(hipMalloc(&w->queues, mrt::kMaxQueues * mrt::kQueueStrideWords * sizeof(unsigned)));
         MRT_HIP(hipMalloc(&w->status, 64 * sizeof(int)));
         MRT_HIP(hipMemset(w->status, 0, 64 * sizeof(int)));
+#ifdef MRT_DONE_EVENT
         MRT_HIP(hipEventCreateWithFlags(&w->done, mrt::kDoneEventFlags));
+#endif
     }
     w->lastUse = ++useClock;
     const size_t need = (size_t)(stackCap - ldsStack) * (size_t)totalLanes;
@@ -452,7 +469,7 @@ mrt_launch_cfg tune_candidate(const mrt_launch_cfg& base, int c, int stage1) {
         mrt_launch_cfg x = tune_candidate(base, stage1, stage1);
         const int k = c - TuneState::kSchedules;
         if (k < 2 && base.spec_slack == kDefaultSpecSlack) x.spec_slack = k == 0 ? 4 : 6;
-        if (k == 2 && base.tail_lanes == kDefaultTailLanes) x.tail_lanes = 0;
+        if (k == 2 && base.tail_lanes == kDefaultTailLanes) x.tail_lanes = kDefaultTailLanes ? 0 : kTunedTailLanes;
         return x;
     }
     mrt_launch_cfg x = base;
@@ -632,10 +649,10 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     if (info) MRT_HIP(hipEventRecord(t->evStart, s));
     if (slot) MRT_HIP(hipEventRecord(slot->start, s));
     MRT_HIP(mrt::launch_trace(v, a, blocks, s));
-#ifndef MRT_NO_DONE_EVENT
+#ifdef MRT_DONE_EVENT
     MRT_HIP(hipEventRecord(ws->done, s));
-    ws->launched = true;
 #endif
+    ws->launched = true;
     if (slot) {
         MRT_HIP(hipEventRecord(slot->stop, s));
         slot->cand = cand;

@@ -96,7 +96,7 @@ typedef struct mrt_launch_cfg {
                                   of each batch size (per kernel variant, up to 64 sizes) time eight ray-
                                   distribution schedules (static rounds at 20, 16, 12 or 8 waves/CU, per-XCD
                                   queues with spec_slack 2 or 4, the global queue at 16 or 12 waves/CU), then
-                                  the winner with spec_slack 4 and 6 and without the cooperative tail (each
+                                  the winner with spec_slack 4 and 6 and with the cooperative tail (each
                                   knob only when left at its default), eight times each without blocking,
                                   after one untimed round of them; the median ranks them and a candidate
                                   replaces the fixed rule (stage 1) or the stage-1 winner (stage 2) only
@@ -106,7 +106,8 @@ typedef struct mrt_launch_cfg {
     int32_t tail_lanes;        /* exact 4-wide speculative traversal: a wave that cannot refill (its strided
                                   round, or its queue drained) and is down to at most this many tracing
                                   lanes finishes those rays four lanes per ray, one node or up to four
-                                  triangles per ray per memory round trip (0..16; 0 = off; -1 = default) */
+                                  triangles per ray per memory round trip (0..16; 0 = off, the default;
+                                  -1 = default; the autotuner tries 16 when left at the default) */
     int32_t steal;             /* queue modes (num_queues >= 2): 1 = a wave whose XCD's queue is dry takes rays
                                   from the back of the other queues (one 64-bit atomic per wave refill; the
                                   owners keep taking from the front, so each XCD stays on its own Morton

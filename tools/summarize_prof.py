@@ -21,7 +21,7 @@ import sys
 
 src, tag = sys.argv[1], sys.argv[2]
 repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-dst = os.path.join(repo, "profiles")
+dst = sys.argv[3] if len(sys.argv) > 3 else os.path.join(repo, "profiles")   # the GPU box: under gpurun_out/
 os.makedirs(dst, exist_ok=True)
 shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
 

@@ -7,7 +7,7 @@ steady state instead: the GPU is warmed first, each candidate is locked in turn
 (mrt_tracer_tune_import) and timed over interleaved rounds of back-to-back launches
 (HIP events), and the library's own rule picks the winner — stage 1 over the eight
 ray-distribution schedules against the fixed rule, stage 2 over the winner's
-spec_slack 4 / 6 / no-tail variants, a challenger replacing the incumbent only when
+spec_slack 4 / 6 / cooperative-tail variants, a challenger replacing the incumbent only when
 its median is 3 % faster (mrt_api.cpp kTuneMargin).
 
   python tools/tune_db.py [--workload W ...] [--rounds 5] [--launches 20] [--out PATH]
@@ -27,7 +27,7 @@ MARGIN = 0.03
 N_SCHEDULES, STAGE2 = 8, 3
 
 
-def variant_key(any_hit, exact, lds_stack=16, nodes=1, tail=True):
+def variant_key(any_hit, exact, lds_stack=16, nodes=1, tail=False):
     """mrt_api.cpp variant_key() of a speculative, stats-free launch."""
     return int(any_hit) | 2 | (4 if exact else 0) | ({8: 0, 16: 1, 32: 2}[lds_stack] << 4) | (nodes << 6) | (256 if tail else 0)
 
