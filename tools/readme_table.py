@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--parity-rays", type=int, default=16384)
     ap.add_argument("--cells", default="", help="comma-separated subset of workloads")
     ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out"))
+    ap.add_argument("--tune-db", default=None, help="saved schedules to lock (default: the package's)")
     args = ap.parse_args()
 
     import numpy as np
@@ -61,8 +62,10 @@ def main():
     import oracle_lib as O
     from mrt.tracer import Tracer
 
+    from mrt.schedules import DEFAULT_PATH, ScheduleStore
     torch.cuda.set_device(0)
     tracer = Tracer(0)
+    bench.STORE = ScheduleStore(args.tune_db or DEFAULT_PATH)   # cells without saved schedules autotune in warmup
     want = set(args.cells.split(",")) if args.cells else None
     state = {"cell": "start", "t0": time.perf_counter()}
     stop = threading.Event()
@@ -102,6 +105,7 @@ def main():
             "bvh_mb": round(4 * (len(bufs[0]) + len(bufs[1]) + len(bufs[2])) / 2**20, 1), "build_s": round(build_s, 1),
             "per_ray": {"nodes": round(n_nodes / batches.rays_traced, 2), "tris": round(n_tris / batches.rays_traced, 2)},
             "alg_gbs": round(alg_bytes / (kernel_ms * 1e-3) / 1e9, 1),
+            "schedule": bench.schedule_of(tracer, batches.batches[0][0], True)["name"],
             "parity_rays": n, "parity_agree": agree, "parity_kind": "hit/miss" if any_hit else "id+t exact",
         }
         rows.append(row)
@@ -124,15 +128,17 @@ README_INNER_NODES = {"bunny": 50876, "dragon": 301376, "conference": 105025, "h
 
 
 def write_md(rows, out):
+    # alg. GB/s: SURVEY §8(d)'s bytes per ray (cache hits included) over the kernel time; a rate, not a level's
+    # traffic, so it may exceed the HBM peak (bench.py's roofline prices the per-level PMC bytes instead)
     md = ["| README cell | tris (stand-in) | inner nodes (stand-in / README) | README Mrays/s | MI355X Mrays/s | "
-          "× README | kernel ms | nodes/ray | tris/ray | alg. GB/s | oracle agreement |",
-          "|---|---|---|---|---|---|---|---|---|---|---|"]
+          "× README | kernel ms | nodes/ray | tris/ray | alg. GB/s (not a roofline) | schedule | oracle agreement |",
+          "|---|---|---|---|---|---|---|---|---|---|---|---|"]
     for r in rows:
         ref = README_INNER_NODES.get(r["workload"].split("-")[0])
         nodes = f"{r['inner_nodes']:,} / {ref:,}" if ref else f"{r['inner_nodes']:,} / —"
         md.append(f"| {r['workload']} (README:{r['readme_line']}) | {r['tris']:,} | {nodes} | {r['readme_mrays']} | "
                   f"**{r['mrays']}** | {r['x_readme']} | {r['kernel_ms']} | {r['per_ray']['nodes']} | "
-                  f"{r['per_ray']['tris']} | {r['alg_gbs']} | {r['parity_agree']:.4f} ({r['parity_kind']}, "
+                  f"{r['per_ray']['tris']} | {r['alg_gbs']} | {r.get('schedule', '')} | {r['parity_agree']:.4f} ({r['parity_kind']}, "
                   f"{r['parity_rays']} rays) |")
     with open(os.path.join(out, "readme_table.md"), "w") as f:
         f.write("\n".join(md) + "\n")

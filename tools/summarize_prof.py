@@ -26,6 +26,11 @@ os.makedirs(dst, exist_ok=True)
 shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
 
 
+def grid_of(row):
+    """Grid size in threads of a kernel-trace or counter-collection row (the two CSVs name it differently)."""
+    return int(row["Grid_Size"]) if "Grid_Size" in row else int(row["Grid_Size_X"])
+
+
 def bench_line(log):
     for line in open(log):
         if line.startswith("{"):
@@ -43,7 +48,7 @@ timed = max((r for r in stats if "trace_kernel" in r["Name"]), key=lambda r: int
 durs = []
 for f in glob.glob(os.path.join(src, "kt", "run_kernel_trace.csv")):
     for r in csv.DictReader(open(f)):
-        if r["Kernel_Name"] == timed["Name"] and (grid is None or int(r["Grid_Size"]) == grid):
+        if r["Kernel_Name"] == timed["Name"] and (grid is None or grid_of(r) == grid):
             durs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 out = {"kernel": timed["Name"], "calls": int(timed["Calls"]), "avg_ns_all_calls": float(timed["AverageNs"]),
        "timed_grid_calls": len(durs), "avg_ns": (sum(durs) / len(durs)) if durs else float(timed["AverageNs"]),
@@ -53,9 +58,9 @@ for p in sorted(d for d in os.listdir(src) if d.startswith("pmc")):
     rows = list(csv.DictReader(open(os.path.join(src, p, "run_counter_collection.csv"))))
     vals = collections.defaultdict(list)
     for r in rows:
-        if r["Kernel_Name"] == timed["Name"] and (grid is None or int(r["Grid_Size"]) == grid):
+        if r["Kernel_Name"] == timed["Name"] and (grid is None or grid_of(r) == grid):
             vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-            out.update({"grid_size": int(r["Grid_Size"]), "lds": int(r["LDS_Block_Size"])})
+            out.update({"grid_size": grid_of(r), "lds": int(r["LDS_Block_Size"])})
     for k, v in vals.items():
         out["pmc"][k] = {"per_launch_mean": sum(v) / len(v), "launches": len(v)}
 pm = {k: v["per_launch_mean"] for k, v in out["pmc"].items()}
