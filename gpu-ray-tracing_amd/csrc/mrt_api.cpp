@@ -208,7 +208,6 @@ mrt_launch_cfg default_cfg() {
     c.static_rounds = 1;
     c.autotune = kDefaultAutotune;
     c.tail_lanes = kDefaultTailLanes;
-    c.steal = 0;
     return c;
 }
 
@@ -219,7 +218,7 @@ bool valid_cfg(const mrt_launch_cfg& c) {
            c.lane_groups >= 1 && c.lane_groups <= 64 && (c.lane_groups & (c.lane_groups - 1)) == 0 &&
            (c.wide >= 0 && c.wide <= 2) && c.spec_slack >= 0 && c.spec_slack <= 63 &&
            c.static_rounds >= 1 && c.static_rounds <= 64 && (c.autotune == 0 || c.autotune == 1) &&
-           c.tail_lanes >= 0 && c.tail_lanes <= 16 && (c.steal == 0 || c.steal == 1);
+           c.tail_lanes >= 0 && c.tail_lanes <= 16;
 }
 
 // The cooperative tail runs in the exact 4-wide kernels whose leaf refs carry counts.
@@ -633,7 +632,6 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     a.totalLanes = totalLanes;
     a.stackCap = stackCap;
     a.tailLanes = cfg.tail_lanes;
-    a.steal = a.numQueues >= 2 ? cfg.steal : 0;
     a.queues = ws->queues;
     a.spill = ws->spill;
     // The blocking call counts this launch's overflows in a slot of its own; the
@@ -840,7 +838,6 @@ int mrt_tracer_set_config(mrt_tracer* t, const mrt_launch_cfg* cfg) {
     if (c.static_rounds == 0) c.static_rounds = d.static_rounds;
     if (c.autotune < 0) c.autotune = d.autotune;
     if (c.tail_lanes < 0) c.tail_lanes = d.tail_lanes;
-    if (c.steal < 0) c.steal = d.steal;
     if (!valid_cfg(c)) return fail(MRT_ERR_INVALID_ARG, "launch config out of range");
     std::lock_guard<std::mutex> lock(t->mu);
     t->cfg = c;

@@ -43,7 +43,6 @@ struct TraceArgs {
     int laneGroupsLog2;        // strided mode: a wave's lanes take rays from 2^k spread-out sub-ranges
     int totalLanes;            // grid lanes (stride of the spill slab)
     int stackCap;              // stack entries incl. the sentinel (kStackCapacity, or the wide tree's bound)
-    int steal;                 // queue modes: a dry queue's waves take rays from the back of the others
     int tailLanes;             // exact 4-wide speculative kernels: a wave that cannot refill and is down to
                                // this many live lanes finishes them four lanes per ray (0 = off)
     unsigned* queues;          // numQueues heads, kQueueStrideWords apart, zeroed per launch

@@ -108,10 +108,6 @@ typedef struct mrt_launch_cfg {
                                   lanes finishes those rays four lanes per ray, one node or up to four
                                   triangles per ray per memory round trip (0..16; 0 = off, the default;
                                   -1 = default; the autotuner tries 16 when left at the default) */
-    int32_t steal;             /* queue modes (num_queues >= 2): 1 = a wave whose XCD's queue is dry takes rays
-                                  from the back of the other queues (one 64-bit atomic per wave refill; the
-                                  owners keep taking from the front, so each XCD stays on its own Morton
-                                  range until the end); 0 (default) = no stealing */
 } mrt_launch_cfg;
 
 /* Per-launch statistics reported back to the host (optional). */
