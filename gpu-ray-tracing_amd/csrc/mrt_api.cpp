@@ -456,8 +456,11 @@ int refresh_wide(mrt_tracer* t) {
 // size cycle through these eight candidates, each timed with an event pair that is
 // read back on a later launch (never blocking); after kSamples launches each the
 // fastest is timed again with the speculation slack at 4 and 6 (stage 2), and the
-// fastest of the three is kept for that batch size. Results do not depend on the schedule
-// (closest hits are the same hits; an any-hit ray may report a different valid hit).
+// fastest of the three is kept for that batch size. Closest hits are the same hits under
+// every schedule, except that which of two triangles at exactly the same t wins follows the
+// traversal order, and so can the hit an any-hit ray reports (any valid hit). A
+// reproducible run pins the schedule: autotune 0, or the schedules saved per BVH
+// (mrt_tracer_tune_export / _import, mrt/tuned_schedules.json for the bench).
 constexpr int kMaxTuned = 64;   // batch sizes tuned per handle; others use the rule
 
 mrt_launch_cfg tune_candidate(const mrt_launch_cfg& base, int c, int stage1) {

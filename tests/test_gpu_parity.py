@@ -365,6 +365,57 @@ def test_tail_lanes_keep_results(tracer, wl, tail):
         assert np.array_equal(res[:, :2], want[:, :2])
 
 
+def fuzz_rays(scene, n, seed, w=96, h=72):
+    """Incoherent rays inside a scene (test_random_rays_fuzz's recipe)."""
+    bufs, base, _, _, _ = scene_setup(scene, w, h, "primary")
+    prim, _, _ = O.trace(base, *bufs)
+    hits = np.nonzero(prim[:, 0] >= 0)[0]
+    rng = np.random.default_rng(seed)
+    pick = rng.choice(hits, n)
+    t = prim[pick, 1].view(np.float32)
+    p = base[pick, 0:3] + base[pick, 4:7] * t[:, None]
+    extent = float(np.ptp(p, axis=0).max())
+    rays = np.empty((n, 8), np.float32)
+    rays[:, 0:3] = p + rng.normal(0.0, 0.05 * extent, (n, 3))
+    d = rng.normal(size=(n, 3))
+    rays[:, 4:7] = d / np.linalg.norm(d, axis=1, keepdims=True)
+    rays[:, 3] = np.where(rng.random(n) < 0.5, 0.0, rng.uniform(0.0, 0.01 * extent, n))
+    rays[:, 7] = np.where(rng.random(n) < 0.2, np.inf, rng.uniform(0.05, 2.0, n) * extent)
+    return bufs, rays
+
+
+@pytest.mark.parametrize("scene", ["bunny", "hairball:800", "sibenik"])
+def test_frontier_tail_group_widths(tracer, scene):
+    """The frontier tail gives a wave's last R <= 16 rays 64/R lanes each (F = 16/R entries
+    per round trip) and widens the groups as rays finish. Batches of 1..64 rays land in
+    one wave, so every group width (4..64 lanes), the regroups, the window's overflow onto
+    the home stack and the pops back from it all run: closest hits bit-identical to the
+    oracle, any hits genuine with the same hit/miss, no stack overflow."""
+    from mrt.tracer import GpuBvh, RayBuffer
+    bufs, rays = fuzz_rays(scene, 1200, 7)
+    want = {a: O.trace(rays, *bufs, any_hit=a, threads=8)[0] for a in (False, True)}
+    saved = tracer.config()
+    try:
+        tracer.set_config(wide=1, tail_lanes=16, autotune=0)
+        tracer.set_bvh(GpuBvh(bufs))
+        lo = 0
+        for n in (1, 2, 3, 4, 5, 7, 8, 9, 15, 16, 17, 31, 33, 64, 1, 1, 2, 3):
+            for any_hit in (False, True):
+                rb = RayBuffer(rays[lo:lo + n], need_closest_hit=not any_hit)
+                rb.results.fill_(0x5A5A5A5A)
+                tracer.trace_batch(rb, exact_rcp=True)
+                res = rb.results_numpy()
+                assert tracer.last_info["stack_overflows"] == 0
+                assert (res[:, 2:] == 0x5A5A5A5A).all()
+                if any_hit:
+                    assert_valid_hits(rays[lo:lo + n], res, want[True][lo:lo + n], bufs)
+                else:
+                    assert np.array_equal(res[:, :2], want[False][lo:lo + n, :2]), f"batch of {n} at {lo}"
+            lo += n
+    finally:
+        tracer.set_config(**saved)
+
+
 def test_timed_trace_keeps_async_overflow_count(tracer):
     """a blocking trace counts its own overflows in a slot of its own; the
     sticky counter of earlier asynchronous launches on the stream is not reset by it."""
