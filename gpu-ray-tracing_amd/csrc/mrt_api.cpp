@@ -75,8 +75,8 @@ struct mrt_tracer {
 // Launch-schedule autotuning state of one (batch size, kernel variant).
 struct TuneState {
     // Stage 1: kSchedules ray-distribution schedules; stage 2: the stage-1 winner
-    // with the speculation slack at 4 and 6, and with the cooperative tail (without it
-    // if the tracer's default has it) (candidates kSchedules .. kSchedules + 2).
+    // with the speculation slack at 4 and 6, and without the frontier tail (with it if
+    // the tracer's default is off) (candidates kSchedules .. kSchedules + 2).
     static constexpr int kSchedules = 8;
     static constexpr int kStage2 = 3;
     static constexpr int kCandidates = kSchedules + kStage2;
@@ -187,12 +187,15 @@ constexpr int kDefaultSpecSlack = 2;
 // Launch schedules are tuned per batch size (autotune_*, below): equal or faster on
 // every workload once settled (+9...+16 % on bunny/dragon primary batches).
 constexpr int kDefaultAutotune = 1;
-// The cooperative tail (trace_kernel.hip cooperative_tail): at most this many live
-// lanes of a wave that cannot refill finish four lanes per ray.
+// The frontier tail (trace_kernel.hip frontier_tail): a wave that cannot refill and is
+// down to at most this many live lanes finishes them 64/R lanes per ray. On by default:
+// hairball diffuse 640x480 0.314 -> 0.225 ms, Mori AO 0.055 -> 0.044, bunny primary
+// +5 %; conference AO and sponza diffuse lose 2-4 % (profiles/round3_frontier_ab.txt),
+// where the autotuner's stage 2 can turn it off.
 #ifndef MRT_DEFAULT_TAIL_LANES
-#define MRT_DEFAULT_TAIL_LANES 0
+#define MRT_DEFAULT_TAIL_LANES 16
 #endif
-// What the autotuner's stage 2 tries when tail_lanes is left at its default (0).
+// What the autotuner's stage 2 tries when tail_lanes is left at its default (16: off).
 constexpr int kTunedTailLanes = 16;
 constexpr int kDefaultTailLanes = MRT_DEFAULT_TAIL_LANES;
 
@@ -221,7 +224,7 @@ bool valid_cfg(const mrt_launch_cfg& c) {
            c.tail_lanes >= 0 && c.tail_lanes <= 16;
 }
 
-// The cooperative tail runs in the exact 4-wide kernels whose leaf refs carry counts.
+// The frontier tail runs in the exact 4-wide kernels whose leaf refs carry counts.
 bool with_tail(const mrt_tracer* t, const mrt::TraceVariant& v, const mrt_launch_cfg& c) {
     return c.tail_lanes > 0 && v.nodes == mrt::kNodeWide4 && t->wideLeafCounts;
 }
@@ -466,7 +469,7 @@ constexpr int kMaxTuned = 64;   // batch sizes tuned per handle; others use the 
 mrt_launch_cfg tune_candidate(const mrt_launch_cfg& base, int c, int stage1) {
     if (c >= TuneState::kSchedules) {
         // stage 2: the stage-1 winner, the wave turning to its leaves once <= 4 (6) lanes
-        // still search, or without the cooperative tail (only for knobs the caller left
+        // still search, or with the frontier tail toggled (only for knobs the caller left
         // at their defaults)
         mrt_launch_cfg x = tune_candidate(base, stage1, stage1);
         const int k = c - TuneState::kSchedules;

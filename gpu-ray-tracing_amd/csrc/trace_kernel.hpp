@@ -44,7 +44,7 @@ struct TraceArgs {
     int totalLanes;            // grid lanes (stride of the spill slab)
     int stackCap;              // stack entries incl. the sentinel (kStackCapacity, or the wide tree's bound)
     int tailLanes;             // exact 4-wide speculative kernels: a wave that cannot refill and is down to
-                               // this many live lanes finishes them four lanes per ray (0 = off)
+                               // this many live lanes finishes them in the frontier tail (0 = off)
     unsigned* queues;          // numQueues heads, kQueueStrideWords apart, zeroed per launch
     int* spill;                // (stackCap - S) * totalLanes ints
     int* status;               // [0] = stack overflow count (lanes that pushed past kStackCapacity)
@@ -63,7 +63,7 @@ struct TraceVariant {
     bool stats;
     int ldsStack;       // 8, 16 or 32 LDS entries per lane
     int nodes = 0;      // kNodeCompact2, or a 4-wide form derived from it (speculative mode only)
-    bool tail = false;  // kNodeWide4 with leaf counts: the instantiation with the cooperative tail
+    bool tail = false;  // kNodeWide4 with leaf counts: the instantiation with the frontier tail
 };
 
 // The 4-wide node array derived from a Compact2 node array (numNodes inner nodes,

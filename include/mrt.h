@@ -96,7 +96,7 @@ typedef struct mrt_launch_cfg {
                                   of each batch size (per kernel variant, up to 64 sizes) time eight ray-
                                   distribution schedules (static rounds at 20, 16, 12 or 8 waves/CU, per-XCD
                                   queues with spec_slack 2 or 4, the global queue at 16 or 12 waves/CU), then
-                                  the winner with spec_slack 4 and 6 and with the cooperative tail (each
+                                  the winner with spec_slack 4 and 6 and without the frontier tail (each
                                   knob only when left at its default), eight times each without blocking,
                                   after one untimed round of them; the median ranks them and a candidate
                                   replaces the fixed rule (stage 1) or the stage-1 winner (stage 2) only
@@ -105,9 +105,10 @@ typedef struct mrt_launch_cfg {
                                   _import save and restore the choices). 0 = the fixed rule only; -1 = default */
     int32_t tail_lanes;        /* exact 4-wide speculative traversal: a wave that cannot refill (its strided
                                   round, or its queue drained) and is down to at most this many tracing
-                                  lanes finishes those rays four lanes per ray, one node or up to four
-                                  triangles per ray per memory round trip (0..16; 0 = off, the default;
-                                  -1 = default; the autotuner tries 16 when left at the default) */
+                                  lanes finishes those rays in the frontier tail: 64/R lanes per ray for R
+                                  rays (at least four), up to 16/R pending nodes or four-triangle leaf chunks
+                                  per ray per memory round trip, regrouping as rays finish (0..16; 0 = off;
+                                  default 16; -1 = default; the autotuner tries 0 when left at the default) */
 } mrt_launch_cfg;
 
 /* Per-launch statistics reported back to the host (optional). */

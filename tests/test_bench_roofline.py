@@ -69,4 +69,4 @@ def test_schedule_names():
     assert bench.schedule_name(-1) == "fixed rule"
     assert bench.schedule_name(2) == bench.SCHEDULES[2]
     assert bench.schedule_name(8 | (3 << 8)).endswith("spec_slack 4")
-    assert bench.schedule_name(10 | (0 << 8)).endswith("cooperative tail")
+    assert bench.schedule_name(10 | (0 << 8)).endswith("no frontier tail")

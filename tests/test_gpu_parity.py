@@ -320,11 +320,11 @@ def test_stack_overflow_is_reported(tracer, depth, overflow):
 
 @pytest.mark.parametrize("rays_n", [1, 5, 16, 17, 40])
 @pytest.mark.parametrize("depth", [10, 40, 63, 70])
-def test_cooperative_tail_on_deep_stacks(tracer, depth, rays_n):
-    """The cooperative tail (cfg.tail_lanes) takes a wave's last <= 16 rays four lanes
-    per ray; their stacks stay in the home lanes' LDS and spill columns. A batch of a
-    few comb rays enters it at once and pushes through the spill slab: the hand
-    answer for every ray, closest and any hit."""
+def test_frontier_tail_on_deep_stacks(tracer, depth, rays_n):
+    """The frontier tail (cfg.tail_lanes) takes a wave's last <= 16 rays 64/R lanes per
+    ray; their stacks stay in the home lanes' LDS and spill columns. A batch of a few
+    comb rays enters it at once and pushes through the spill slab: the hand answer for
+    every ray, closest and any hit."""
     from mrt.tracer import GpuBvh, RayBuffer
     bufs, ray, expect = kat.scene_comb(depth)
     saved = tracer.config()
@@ -349,9 +349,10 @@ def test_cooperative_tail_on_deep_stacks(tracer, depth, rays_n):
 @pytest.mark.parametrize("wl", WORKLOADS, ids=lambda w: "-".join(map(str, w)))
 @pytest.mark.parametrize("tail", [0, 16])
 def test_tail_lanes_keep_results(tracer, wl, tail):
-    """Closest hits bit-identical to the oracle with the cooperative tail off and at
-    its widest (the tail tests the same leaves; within a leaf the first of equal t
-    wins, as in the sequential loop); any hit: genuine hits, same hit/miss."""
+    """Closest hits bit-identical to the oracle with the frontier tail off and at its
+    widest (the tail tests the leaves that can hold the closest hit; within a step the
+    first of equal t in list order wins, as in the sequential loop); any hit: genuine
+    hits, same hit/miss."""
     bufs, rays, any_hit, want, _ = scene_setup(*wl)
     saved = tracer.config()
     try:

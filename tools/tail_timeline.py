@@ -50,6 +50,15 @@ def main():
               f"{tail.sum()} of {len(end)} rays finished in the tail", flush=True)
         for q in (50, 90, 99, 99.9, 100):
             print(f"   {q:5}% of rays done by {np.percentile(end, q):7.1f} us")
+        # the last fetch: the queue (or the strided rounds) ran dry here; what was in flight then
+        dry = start.max()
+        fl = (start <= dry) & (end > dry)
+        print(f"   last ray fetched at {dry:.1f} us ({100.0 * (end <= dry).mean():.1f} % done by then, {fl.sum()} in "
+              f"flight); drain {end.max() - dry:.1f} us; in flight at +10/+25/+50/+100 us: "
+              + " ".join(str(int(((start <= dry + d) & (end > dry + d)).sum())) for d in (10, 25, 50, 100)))
+        if tail.any():
+            print(f"   tail entries after the last fetch: {int((entry[tail] > dry).sum())} of {tail.sum()}; "
+                  f"rays in flight at the last fetch that end in the tail: {int((fl & tail).sum())}")
         if tail.any():
             per = (end[tail] - entry[tail]) / np.maximum(1, iters[tail])
             print(f"   tail entries: median {np.nanmedian(entry):.1f} us, 90% by {np.nanpercentile(entry, 90):.1f}, "

@@ -5,10 +5,10 @@ The in-library autotuner ranks candidates from ~100 launches interleaved with ea
 other, early in a process while clocks still ramp; here every candidate is timed in
 steady state instead: the GPU is warmed first, each candidate is locked in turn
 (mrt_tracer_tune_import) and timed over interleaved rounds of back-to-back launches
-(HIP events), and the library's own rule picks the winner — stage 1 over the eight
-ray-distribution schedules against the fixed rule, stage 2 over the winner's
-spec_slack 4 / 6 / cooperative-tail variants, a challenger replacing the incumbent only when
-its median is 3 % faster (mrt_api.cpp kTuneMargin).
+(HIP events): the eight ray-distribution schedules, each also with every stage-2
+modifier (spec_slack 4 / 6, the frontier tail toggled), then the two fastest against the
+fixed rule again; a challenger replaces the rule only when its median is 3 % faster
+(mrt_api.cpp kTuneMargin).
 
   python tools/tune_db.py [--workload W ...] [--rounds 5] [--launches 20] [--out PATH]
 """
@@ -58,7 +58,9 @@ def main():
         b = bench.Batches(wl, e["scene"], e["gbvh"], tracer)
         for exact in ([True, False] if args.fast_rcp else [True]):
             launches = [tracer.launcher(rb, exact_rcp=exact) for rb, _ in b.batches]
-            keys = sorted({(rb.size, variant_key(not rb.need_closest_hit, exact)) for rb, _ in b.batches})
+            cfg = tracer.config()
+            tail = cfg["tail_lanes"] > 0 and cfg["wide"] == 1   # the library's with_tail()
+            keys = sorted({(rb.size, variant_key(not rb.need_closest_hit, exact, tail=tail)) for rb, _ in b.batches})
 
             def lock(code):
                 tracer.load_schedules([(n, v, code, _lib.MRT_TUNE_VERSION) for n, v in keys])
@@ -96,19 +98,24 @@ def main():
             cus = torch.cuda.get_device_properties(0).multi_processor_count
             big = g.node_bytes + g.woop_bytes > bench.MALL_BYTES
             rule_c = 0 if not big else (4 if b.batches[0][0].size <= 3 * cus * 16 * 64 else 3)
-            s1 = timed(list(range(N_SCHEDULES)))
+            # every schedule, and every schedule with each stage-2 modifier (spec_slack 4, 6, the
+            # frontier tail toggled): the in-library tuner only modifies its stage-1 winner, which
+            # misses e.g. per-XCD queues without the tail on bunny primary 1024x768
+            codes = list(range(N_SCHEDULES)) + [(N_SCHEDULES + k) | (c << 8) for c in range(N_SCHEDULES)
+                                                for k in range(STAGE2)]
+            s1 = timed(codes)
             best = min(s1, key=s1.get)
-            stage1 = best if s1[best] < (1 - MARGIN) * s1[rule_c] else rule_c
-            s2 = timed([stage1] + [(N_SCHEDULES + k) | (stage1 << 8) for k in range(STAGE2)])
-            inc = stage1
+            # the two best against each other again (the sweep's medians are one sample each)
+            top2 = sorted(s1, key=s1.get)[:2]
+            s2 = timed(sorted(set([rule_c] + top2)))
             best2 = min(s2, key=s2.get)
-            chosen = best2 if s2[best2] < (1 - MARGIN) * s2[inc] else inc
+            chosen = best2 if s2[best2] < (1 - MARGIN) * s2[rule_c] else rule_c
             lock(chosen)
             store.update(e["gbvh"].fingerprint, tracer.schedules())
-            print(f"{wl} exact={exact}: rule {rule_c} {s1[rule_c]:.4f} ms; stage 1 "
-                  + " ".join(f"{c}:{v:.4f}" for c, v in s1.items())
-                  + f" -> {stage1}; stage 2 " + " ".join(f"{c & 0xff}:{v:.4f}" for c, v in s2.items())
-                  + f" -> {chosen & 0xff} ({bench.schedule_name(chosen)})", flush=True)
+            print(f"{wl} exact={exact}: rule {rule_c} {s1[rule_c]:.4f} ms; sweep "
+                  + " ".join(f"{c & 0xff}/{c >> 8}:{v:.4f}" for c, v in sorted(s1.items(), key=lambda kv: kv[1])[:6])
+                  + "; final " + " ".join(f"{c & 0xff}/{c >> 8}:{v:.4f}" for c, v in s2.items())
+                  + f" -> {chosen & 0xff}/{chosen >> 8} ({bench.schedule_name(chosen)})", flush=True)
     store.save(out)
     print(f"wrote {out}")
 
