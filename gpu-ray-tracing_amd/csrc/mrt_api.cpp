@@ -282,7 +282,10 @@ int variant_key(const mrt::TraceVariant& v) {
 // rounds: there the same queue costs up to 2.6x (contended atomics).
 constexpr int64_t kMallBytes = 256ll << 20;
 constexpr int kBigQueueThreshold = 48;
-constexpr int kBigQueueWaves = 16;
+#ifndef MRT_BIG_QUEUE_WAVES
+#define MRT_BIG_QUEUE_WAVES 16
+#endif
+constexpr int kBigQueueWaves = MRT_BIG_QUEUE_WAVES;
 constexpr int kBigQueueWavesSmall = 12;
 constexpr int kBigQueueSmallRaysPerLane = 3;   // of the 16-wave grid
 
@@ -485,7 +488,7 @@ mrt_launch_cfg tune_candidate(const mrt_launch_cfg& base, int c, int stage1) {
         case 0: break;                                                      // static rounds, 20 waves/CU
         case 1: x.waves_per_cu = 8; break;                                  // static rounds, fewer waves
         case 2: x.num_queues = 8; break;                                    // per-XCD queues
-        case 3: x.num_queues = 1; x.fetch_threshold = 48; x.waves_per_cu = 16; break;   // global queue
+        case 3: x.num_queues = 1; x.fetch_threshold = kBigQueueThreshold; x.waves_per_cu = kBigQueueWaves; break;   // global queue
         case 4: x.num_queues = 1; x.fetch_threshold = 48; x.waves_per_cu = 12; break;
         case 5: x.waves_per_cu = 16; break;
         case 6: x.waves_per_cu = 12; break;
