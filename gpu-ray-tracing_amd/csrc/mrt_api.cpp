@@ -492,9 +492,12 @@ mrt_launch_cfg tune_candidate(const mrt_launch_cfg& base, int c, int stage1) {
         case 4: x.num_queues = 1; x.fetch_threshold = 48; x.waves_per_cu = 12; break;
         case 5: x.waves_per_cu = 16; break;
         case 6: x.waves_per_cu = 12; break;
-        default:   // per-XCD queues, the wave leaving for its leaves once <= 4 lanes still search
-            x.num_queues = 8;
-            if (base.spec_slack == kDefaultSpecSlack) x.spec_slack = 4;
+        default:   // the global queue at full occupancy: a lone multi-million-ray launch over a BVH
+                   // above the Infinity Cache (hairball 2 M rays 0.728 -> 0.712 ms), whose frontier
+                   // tail drains it; slower when launches overlap on two streams (the rule's 16)
+            x.num_queues = 1;
+            x.fetch_threshold = kBigQueueThreshold;
+            x.waves_per_cu = kStridedWaves;
             break;
     }
     return x;

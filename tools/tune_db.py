@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--fast-rcp", action="store_true", help="tune the v_rcp_f32 variant too")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--margin", type=float, default=MARGIN,
+                    help="how much faster (median) a candidate must be to replace the rule (the library's 3 %%)")
     args = ap.parse_args()
     import torch
     import bench
@@ -109,7 +111,7 @@ def main():
             top2 = sorted(s1, key=s1.get)[:2]
             s2 = timed(sorted(set([rule_c] + top2)))
             best2 = min(s2, key=s2.get)
-            chosen = best2 if s2[best2] < (1 - MARGIN) * s2[rule_c] else rule_c
+            chosen = best2 if s2[best2] < (1 - args.margin) * s2[rule_c] else rule_c
             lock(chosen)
             store.update(e["gbvh"].fingerprint, tracer.schedules())
             print(f"{wl} exact={exact}: rule {rule_c} {s1[rule_c]:.4f} ms; sweep "
