@@ -208,7 +208,7 @@ def test_exact_reciprocal_is_correctly_rounded_for_every_float(tracer):
                                  dict(waves_per_cu=4, lds_stack=8, num_queues=3),
                                  dict(lds_stack=32, waves_per_cu=4, fetch_threshold=48),
                                  dict(num_queues=1, fetch_threshold=48, waves_per_cu=16), dict(lane_groups=2),
-                                 dict(lane_groups=8), dict(lane_groups=64, waves_per_cu=4), dict(spec_slack=0),
+                                 dict(lane_groups=8), dict(lane_groups=16), dict(lane_groups=64, waves_per_cu=4), dict(spec_slack=0),
                                  dict(spec_slack=63), dict(spec_slack=7, num_queues=2, fetch_threshold=40),
                                  dict(tail_lanes=0), dict(tail_lanes=1), dict(tail_lanes=4),
                                  dict(tail_lanes=16, waves_per_cu=4), dict(tail_lanes=16, lds_stack=8),

@@ -6,7 +6,7 @@ other, early in a process while clocks still ramp; here every candidate is timed
 steady state instead: the GPU is warmed first, each candidate is locked in turn
 (mrt_tracer_tune_import) and timed over interleaved rounds of back-to-back launches
 (HIP events): the eight ray-distribution schedules, each also with every stage-2
-modifier (spec_slack 4 / 6, the frontier tail toggled), then the two fastest against the
+modifier (spec_slack 4 / 6, the frontier tail toggled, 16 lane groups), then the two fastest against the
 fixed rule again; a challenger replaces the rule only when its median is 3 % faster
 (mrt_api.cpp kTuneMargin).
 
@@ -24,7 +24,7 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "gpu-ray-tracing_amd"))
 
 MARGIN = 0.03
-N_SCHEDULES, STAGE2 = 8, 3
+N_SCHEDULES, STAGE2 = 8, 4
 
 
 def variant_key(any_hit, exact, lds_stack=16, nodes=1, tail=False):
