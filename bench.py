@@ -16,19 +16,22 @@ Multi-GPU (torch.distributed.run, one rank per GPU, RCCL): rank 0 builds the
 SBVH and broadcasts the Compact2 buffers, which stay in HBM (the BVH is
 replicated). Two scalings are measured in every run:
 
-  * strong (BASELINE configs[4]): ONE fixed RayBuffer — hairball
-    diffuse 1920x1080 x 8 spp = 16.6 M rays, generated as the reference's
-    Renderer does in <= 2^21-ray batches (Renderer.cc:46, RayGen.cc:124-142) —
-    cut into contiguous shards, one per rank, each traced in <= 2^21-ray
-    launches with no collective; T_n = max over ranks. T_1 is measured in the
-    same run (rank 0 traces the whole buffer alone), eta(n) = T_1 / (n T_n),
-    with and without the RCCL gather of the {id, t} results to rank 0. Reported
-    as "strong_scaling" in every line; with --scaling strong it is the line's value.
-  * weak (the headline value by default): the N-GPU job is N samples per pixel
-    of the workload's view, rank r tracing sample r (rank 0's are the reference's
-    pixel-centre rays, rank r > 0 the r-th Halton (2,3) point in each pixel).
+  * strong (BASELINE configs[4]; the line's value at N > 1): ONE
+    fixed RayBuffer — hairball diffuse 1920x1080 x 8 spp = 16.6 M rays, generated
+    as the reference's Renderer does in <= 2^21-ray batches (Renderer.cc:46,
+    RayGen.cc:124-142) — cut into block-cyclic shards (16 384-ray blocks dealt
+    round-robin to the ranks), each traced in <= 2^21-ray launches with no
+    collective; T_n = max over ranks. T_1 is measured in the same run (rank 0
+    traces the whole buffer alone), eta(n) = T_1 / (n T_n), with and without the
+    RCCL gather of the {id, t} results to rank 0.
+  * weak (the line's value at N = 1, BASELINE configs[1]; a sub-block at N > 1):
+    the N-GPU job is N samples per pixel of the workload's view, rank r tracing
+    sample r (rank 0's are the reference's pixel-centre rays, rank r > 0 the r-th
+    Halton (2,3) point in each pixel).
 
-Rank 0 prints one JSON line.
+Rank 0 prints one JSON line (kept under 10 kB: the headline, its roofline and CPU
+baseline, strong scaling and a few numbers per extra workload); the full per-workload
+detail goes to --detail-out.
 """
 from __future__ import annotations
 
@@ -52,7 +55,9 @@ L2_PEAK_GBS = 34500.0    # the eight XCD L2s together (§L2)
 LINE_BYTES = 128         # gfx950 L1 and L2 line: one TCP_TCC_READ_REQ / TCC_EA0_RDREQ per line
                          # (tools/ubench_levels.hip, profiles/round3_counter_calibration.md)
 MALL_BYTES = 256 << 20   # Infinity Cache: a BVH above this streams from HBM
-PROFILE_TAG = "round3"   # committed rocprofv3 summaries this line cites (profiles/<tag>_<workload>_*)
+PROFILE_TAGS = ("round4", "round3")   # committed rocprofv3 summaries the line may cite, newest first
+                                      # (profiles/<tag>_<workload>_*): only one of the timed schedule is cited
+LINE_MAX_BYTES = 10_000  # the driver parses one stdout line; round 3's 21.7 kB line was not parsed
 STORE = None             # mrt.schedules.ScheduleStore the tracer's schedules are locked from (main())
 LEARNED = None           # ScheduleStore collecting the schedules this run settled (--save-schedules)
 
@@ -122,13 +127,15 @@ def pmc_profile(name, rcp="exact"):
     bytes L2 read over the fabric (TCC_EA0_RDREQ lines: Infinity Cache or HBM) and
     wrote (WRITE_SIZE), the mean kernel duration and the schedule it ran."""
     tag = "" if rcp == "exact" else "_rcpfast"
-    path = os.path.join("profiles", f"{PROFILE_TAG}_{name}{tag}_pmc_summary.json")
-    if not os.path.exists(os.path.join(REPO, path)):
-        return None
-    with open(os.path.join(REPO, path)) as f:
-        s = json.load(f)
-    s["path"] = path
-    return s
+    found = []
+    for ptag in PROFILE_TAGS:
+        path = os.path.join("profiles", f"{ptag}_{name}{tag}_pmc_summary.json")
+        if os.path.exists(os.path.join(REPO, path)):
+            with open(os.path.join(REPO, path)) as f:
+                s = json.load(f)
+            s["path"] = path
+            found.append(s)
+    return found
 
 
 def log(*a):
@@ -518,50 +525,47 @@ def cpu_baseline(batches, bufs, counted, threads, label, fast_results=None):
 
 
 def roofline(name, alg_bytes_per_launch, kernel_ms, bvh_bytes, schedule, rcp="exact"):
-    """Per-level roofline of the dominant kernel. The trace's bytes
-    are served by three levels, each priced against its own ceiling:
-      l2      lines the L1s fetched from L2 (TCP_TCC_READ_REQ x 128 B) / 34.5 TB/s;
-      fabric  lines L2 fetched over the fabric (TCC_EA0_RDREQ x 128 B) + WRITE_SIZE,
-              served by the Infinity Cache or HBM / 8.6 TB/s (the Infinity Cache's
-              random-row rate, above HBM's 8 TB/s, so the bound holds whichever serves them);
-    frac = the larger of the two fractions, `bound` names that level, `achieved` /
-    `peak` are its rate and ceiling, `traffic` = the fabric bytes per launch (an upper
-    bound on HBM bytes: Infinity-Cache hits are counted too) and hbm_measured_frac =
-    traffic / kernel time / 8 TB/s. Rates use this run's kernel time (HIP events);
-    the cited profile must have run the same schedule (autotune candidate and grid)
-    or no level is priced. The algorithmic bytes of SURVEY.md §8(d) (every byte the
-    rays read, cache hits included) are reported beside it, as a rate only: they are
-    not bounded by any one level."""
-    alg = alg_bytes_per_launch / (kernel_ms * 1e-3) / 1e9
-    out = {"bound": None, "achieved": None, "peak": None, "unit": "GB/s", "frac": None, "traffic": None,
-           "kernel_ms": round(kernel_ms, 4), "bvh_bytes": int(bvh_bytes), "bvh_exceeds_mall": bvh_bytes > MALL_BYTES,
-           "algorithmic": {"bytes_per_launch": int(alg_bytes_per_launch), "GBps": round(alg, 1),
-                           "note": "SURVEY §8(d) bytes incl. L1/L2 hits; not a level's traffic"}}
-    prof = pmc_profile(name, rcp)
-    if prof is None:
-        out["note"] = "no committed PMC profile for this workload"
-        return out
+    """Roofline of the dominant kernel, as the bench contract defines it: achieved =
+    the ALGORITHMIC bytes of SURVEY.md §8(d) per launch (every byte the rays read, from
+    the per-ray node/triangle/leaf counts) / this run's HIP-event kernel time, against
+    the 8 TB/s HBM peak; traffic = the bytes the L2s moved over the fabric per launch
+    (rocprofv3 TCC_EA0_RDREQ x 128 B + WRITE_SIZE, calibrated on gfx950 in
+    profiles/round3_counter_calibration.md; Infinity-Cache hits included, so an upper
+    bound on HBM bytes), hbm_measured_frac = traffic / time / 8 TB/s. Cache-resident
+    scenes read most algorithmic bytes from L1/L2, so `frac` can pass 1 there (stated,
+    not clamped: SURVEY §8d). `served` prices what each level actually moved against its
+    own ceiling (L1->L2 requests / 34.5 TB/s; fabric / 8.6 TB/s, the Infinity Cache's
+    random-row rate) and names the larger as `binding_level`. The cited profile must
+    have run the timed schedule (autotune candidate, grid, queues) or none is cited."""
+    t = kernel_ms * 1e-3
+    alg = alg_bytes_per_launch / t / 1e9
+    out = {"bound": "hbm", "achieved": round(alg, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(alg / HBM_PEAK_GBS, 4), "traffic": None,
+           "basis": "SURVEY 8(d) algorithmic bytes per launch / HIP-event kernel time; traffic = PMC fabric bytes",
+           "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": int(alg_bytes_per_launch),
+           "bvh_bytes": int(bvh_bytes), "bvh_exceeds_mall": bvh_bytes > MALL_BYTES}
+    if alg > HBM_PEAK_GBS:
+        out["note"] = "algorithmic rate above the HBM peak: the BVH is cache-resident (L1/L2 hits)"
     want = {k: schedule.get(k) for k in ("autotune_candidate", "grid_waves", "num_queues", "fetch_threshold")}
-    got = {k: (prof.get("schedule") or {}).get(k) for k in want}
-    out["profile"] = {"path": prof["path"], "kernel_ms": round(prof["avg_ns"] / 1e6, 4),
-                      "kernel_ms_ratio": round(prof["avg_ns"] / 1e6 / kernel_ms, 4), "schedule": got}
-    if got != want:
-        out["note"] = f"profile schedule {got} differs from the timed one {want}: not cited"
+    profs = pmc_profile(name, rcp)
+    prof = next((p for p in profs if {k: (p.get("schedule") or {}).get(k) for k in want} == want), None)
+    if prof is None:
+        out["profile"] = {"note": f"no committed PMC profile of the timed schedule {want}",
+                          "seen": [p["path"] for p in profs]}
         return out
     lv = prof["levels"]
-    t = kernel_ms * 1e-3
     levels = {"l2": (lv["l2_request_bytes"], L2_PEAK_GBS), "fabric": (lv["fabric_bytes"], MALL_PEAK_GBS)}
     fr = {k: b / t / 1e9 / peak for k, (b, peak) in levels.items()}
-    bound = max(fr, key=fr.get)
-    b, peak = levels[bound]
-    out.update({"bound": bound, "achieved": round(b / t / 1e9, 1), "peak": peak, "frac": round(fr[bound], 4),
-                "traffic": int(lv["fabric_bytes"]),
-                "levels": {k: {"bytes_per_launch": int(levels[k][0]), "GBps": round(levels[k][0] / t / 1e9, 1),
+    out.update({"traffic": int(lv["fabric_bytes"]),
+                "hbm_measured_GBps": round(lv["fabric_bytes"] / t / 1e9, 1),
+                "hbm_measured_frac": round(lv["fabric_bytes"] / t / 1e9 / HBM_PEAK_GBS, 4),
+                "served": {k: {"bytes_per_launch": int(levels[k][0]), "GBps": round(levels[k][0] / t / 1e9, 1),
                                "peak_GBps": levels[k][1], "frac": round(fr[k], 4)} for k in levels},
+                "binding_level": max(fr, key=fr.get),
                 "l1_hit_fraction_of_algorithmic": round(max(0.0, 1.0 - lv["l2_request_bytes"] / alg_bytes_per_launch), 4),
                 "l2_hit_rate": prof.get("l2_hit_rate"),
-                "hbm_measured_GBps": round(lv["fabric_bytes"] / t / 1e9, 1),
-                "hbm_measured_frac": round(lv["fabric_bytes"] / t / 1e9 / HBM_PEAK_GBS, 4)})
+                "profile": {"path": prof["path"], "kernel_ms": round(prof["avg_ns"] / 1e6, 4),
+                            "kernel_ms_ratio": round(prof["avg_ns"] / 1e6 / kernel_ms, 4)}})
     return out
 
 
@@ -787,14 +791,121 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact):
     }
 
 
+def compact_roofline(rf):
+    """The roofline fields the line keeps (the rest is in the detail file)."""
+    if rf is None:
+        return None
+    keep = {k: rf.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel_ms",
+                                   "hbm_measured_GBps", "hbm_measured_frac", "binding_level", "l2_hit_rate",
+                                   "l1_hit_fraction_of_algorithmic", "alg_bytes_per_launch", "note")
+            if rf.get(k) is not None}
+    if rf.get("served"):
+        keep["served_frac"] = {k: v["frac"] for k, v in rf["served"].items()}
+    prof = rf.get("profile") or {}
+    keep["profile"] = prof.get("path") or prof.get("note")
+    if prof.get("kernel_ms_ratio") is not None:
+        keep["profile_kernel_ms_ratio"] = prof["kernel_ms_ratio"]
+    return keep
+
+
+def compact_parity(cb, fast):
+    out = {"exact_fraction": cb.get("parity_exact_fraction")} if cb else {}
+    if fast and fast.get("parity"):
+        fp = fast["parity"]
+        out["rcp_fast"] = {k: fp[k] for k in ("rays", "mismatch", "tie", "edge", "other", "any_hit_outcome_flips")}
+    return out
+
+
+def compact_workload(r):
+    """One extra workload in the line: value, kernel time, roofline headline numbers,
+    CPU baseline and parity counts."""
+    rf = r.get("roofline") or {}
+    cb = r.get("cpu_baseline")
+    fast = r.get("rcp_fast")
+    out = {"workload": r["workload"], "value": r["value"], "reference_mrays": r.get("reference_mrays"),
+           "kernel_ms": r["kernel_ms_per_launch"], "schedule": (r.get("schedule") or {}).get("name"),
+           "roofline": {k: rf.get(k) for k in ("frac", "hbm_measured_frac", "binding_level", "traffic")},
+           "cpu_baseline": cb and cb["value"], "parity": compact_parity(cb, fast)}
+    if fast:
+        out["rcp_fast_value"] = fast["value"]
+    return out
+
+
+def compact_strong(st):
+    if st is None:
+        return None
+    keep = {k: st[k] for k in ("workload", "rays_traced", "rays_counted", "n_gpus", "shards", "streams", "t1_ms",
+                               "tn_ms", "eta", "gather_ms", "eta_with_gather", "value", "value_with_gather",
+                               "gathered_equals_single_gpu", "collective")}
+    keep["per_rank_ms_max_min"] = [max(st["per_rank_ms"]), min(st["per_rank_ms"])]
+    keep["value_n1_same_run"] = round(st["rays_counted"] / (st["t1_ms"] * 1e-3) / 1e6, 2)
+    if st.get("projected_from_one_gpu"):
+        keep["projected_from_one_gpu"] = {k: {"tn_ms": v["tn_ms"], "eta": v["eta"]}
+                                          for k, v in st["projected_from_one_gpu"].items()}
+    return keep
+
+
+def make_line(args, world, head, extras, strong, tracer_cfg):
+    """(the one stdout line, the full detail). The line stays under LINE_MAX_BYTES
+    (tests/test_bench_line.py builds it from a recorded run)."""
+    ref = REFERENCE_MRAYS.get(args.workload)
+    spec = workload_spec(args.workload)
+    weak = {"workload": args.workload, "value": head["value"], "ms_per_step": head["ms_per_step"],
+            "kernel_ms": head["kernel_ms_per_launch"], "n_gpus": world, "rays_counted_all_ranks":
+            head["rays_counted_all_ranks"], "gather": head.get("gather")}
+    if args.scaling == "strong":
+        value, ms_step = strong["value"], strong["tn_ms"]
+        config = {"workload": strong["workload"], "scene": STRONG["scene"], "width": STRONG["w"],
+                  "height": STRONG["h"], "samples_per_pixel": STRONG["spp"], "rays_total": strong["rays_traced"],
+                  "ray_type": "diffuse", "rcp": args.rcp,
+                  "parallelism": (f"one RayBuffer in {world} block-cyclic shards ({STRONG['block']}-ray blocks "
+                                  f"dealt round-robin to the ranks), BVH replicated, no collective in the step"
+                                  if STRONG["block"] > 0 else f"one RayBuffer in {world} contiguous shards"),
+                  "launch_rays_max": STRONG["max_batch"]}
+        steps = args.strong_steps
+    else:
+        value, ms_step = head["value"], head["ms_per_step"]
+        config = {"workload": args.workload, "scene": spec[0], "scene_tris": head["scene_tris"], "width": spec[1],
+                  "height": spec[2], "ray_type": spec[3], "rays_per_gpu": head["rays_counted"], "rcp": args.rcp,
+                  "parallelism": (f"rays sharded by pixel sample x{world}, BVH replicated "
+                                  f"(weak: one {spec[1]}x{spec[2]} sample per GPU, no collective in the step)")}
+        steps = args.steps
+    config["schedule"] = (head.get("schedule") or {}).get("name") if args.scaling == "weak" else "fixed rule"
+    line = {
+        "metric": METRIC, "value": value, "unit": "Mrays/s", "n_gpus": world, "steps": steps,
+        "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": args.scaling,
+        "vs_baseline": round(head["value"] / ref, 3) if (ref and args.scaling == "weak") else None,
+        "dtype": "f32",
+        "data": "synthetic (deterministic stand-in scene with the README triangle count; rays generated on the device)",
+        "config": config,
+        "roofline": compact_roofline(head["roofline"]) if args.scaling == "weak" else None,
+        "cpu_baseline": ({k: head["cpu_baseline"][k] for k in ("value", "unit", "cores", "kind", "sample", "cpu_model")}
+                         if head.get("cpu_baseline") else None),
+        "parity": compact_parity(head.get("cpu_baseline"), head.get("rcp_fast")),
+        "weak_scaling": weak if args.scaling == "strong" else None,
+        "strong_scaling": compact_strong(strong),
+        "rcp_fast": ({"value": head["rcp_fast"]["value"], "kernel_ms": head["rcp_fast"]["kernel_ms_per_launch"],
+                      "roofline": compact_roofline(head["rcp_fast"]["roofline"])} if head.get("rcp_fast") else None),
+        "autotune_exploration": head.get("autotune_exploration"),
+        "extra_workloads": [compact_workload(r) for r in extras],
+    }
+    if strong is not None and args.scaling == "strong" and strong.get("gathered_equals_single_gpu") is False:
+        line["error"] = "gathered results differ from the single-GPU results"
+    detail = {"args": vars(args), "tracer_config": tracer_cfg, "head": head, "extras": extras, "strong": strong}
+    return line, detail
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20, help="minimum warmup steps (warmup also runs >= 0.3 s)")
     ap.add_argument("--workload", default=HEADLINE, help="a WORKLOADS key or <scene>-<ray>-<W>x<H>")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="which measurement is the line's value (both are reported)")
+    ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
+                    help="which measurement is the line's value (both are reported; default weak at N=1 "
+                         "(BASELINE configs[1]), strong at N>1 (configs[4]))")
+    ap.add_argument("--detail-out", default=os.path.join("gpurun_out", "bench_detail.json"),
+                    help="file for the full per-workload detail ('' = none)")
     ap.add_argument("--rcp", default="exact", choices=["exact", "fast"],
                     help="exact = correctly rounded 1/x (bit-identical to the oracle); fast = v_rcp_f32")
     ap.add_argument("--extra", dest="extra", action="store_true", default=None,
@@ -827,6 +938,9 @@ def main():
     ap.add_argument("--no-explore", action="store_true", help="skip measuring the autotuner's exploration cost")
     ap.add_argument("--no-fast", action="store_true", help="skip the fast-reciprocal (v_rcp_f32) measurement")
     args = ap.parse_args()
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.scaling is None:
+        args.scaling = "weak" if world_env == 1 else "strong"
 
     global STORE, LEARNED
     from mrt.schedules import DEFAULT_PATH, ScheduleStore
@@ -883,48 +997,19 @@ def main():
             f"{ {k: v['eta'] for k, v in (strong['projected_from_one_gpu'] or {}).items()} }")
 
     if rank == 0:
-        ref = REFERENCE_MRAYS.get(args.workload)
-        spec = workload_spec(args.workload)
-        if args.scaling == "strong":
-            value, ms_step = strong["value"], strong["tn_ms"]
-            config = {"workload": strong["workload"], "scene": STRONG["scene"], "width": STRONG["w"],
-                      "height": STRONG["h"], "samples_per_pixel": STRONG["spp"], "rays_total": strong["rays_traced"],
-                      "rcp": args.rcp, "parallelism": f"one RayBuffer in {world} contiguous shards, BVH replicated",
-                      "tracer": tracer.config()}
-        else:
-            value, ms_step = head["value"], head["ms_per_step"]
-            config = {"workload": args.workload, "scene": spec[0], "scene_tris": head["scene_tris"], "width": spec[1],
-                      "height": spec[2], "ray_type": spec[3], "rays_per_gpu": head["rays_counted"], "rcp": args.rcp,
-                      "parallelism": (f"rays sharded by pixel sample x{world}, BVH replicated "
-                                      f"(weak: one {spec[1]}x{spec[2]} sample per GPU, no collective in the step)"),
-                      "tracer": tracer.config()}
-        line = {
-            "metric": METRIC,
-            "value": value,
-            "unit": "Mrays/s",
-            "n_gpus": world,
-            "steps": args.steps if args.scaling == "weak" else args.strong_steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms_step,
-            "higher_is_better": True,
-            "scaling": args.scaling,
-            "vs_baseline": round(head["value"] / ref, 3) if (ref and args.scaling == "weak") else None,
-            "dtype": "f32",
-            "data": "synthetic (deterministic stand-in scene with the README triangle count; rays generated on the device)",
-            "config": config,
-            "roofline": head["roofline"] if args.scaling == "weak" else None,
-            "cpu_baseline": head.get("cpu_baseline"),
-            "strong_scaling": strong,
-            "detail": {k: head[k] for k in ("kernel_ms_per_launch", "rays_traced", "mrays_traced_per_s", "bvh",
-                                            "per_ray", "reference_mrays", "rays_counted_all_ranks", "gather",
-                                            "warmup_steps_run", "schedule", "autotune_exploration")},
-            "rcp_fast": head.get("rcp_fast"),
-            "extra_workloads": [{k: r.get(k) for k in ("workload", "value", "reference_mrays", "kernel_ms_per_launch",
-                                                       "rays_counted", "rays_traced", "per_ray", "roofline", "bvh",
-                                                       "cpu_baseline", "schedule", "rcp_fast", "autotune_exploration")}
-                                for r in extras],
-        }
-        print(json.dumps(line), flush=True)
+        line, detail = make_line(args, world, head, extras, strong, tracer.config())
+        if args.detail_out:
+            os.makedirs(os.path.dirname(os.path.abspath(args.detail_out)), exist_ok=True)
+            with open(args.detail_out, "w") as f:
+                json.dump(detail, f, indent=1)
+            line["detail_file"] = args.detail_out
+        text = json.dumps(line, separators=(",", ":"))
+        if len(text) > LINE_MAX_BYTES:
+            log(f"[line] {len(text)} B > {LINE_MAX_BYTES}: extras dropped from the line (kept in the detail)")
+            line["extra_workloads"] = [{"workload": e["workload"], "value": e["value"]}
+                                       for e in line.get("extra_workloads") or []]
+            text = json.dumps(line, separators=(",", ":"))
+        print(text, flush=True)
         if LEARNED is not None:
             LEARNED.save(args.save_schedules)
             log(f"[schedules] saved {sum(len(v) for v in LEARNED.table.values())} to {args.save_schedules}")

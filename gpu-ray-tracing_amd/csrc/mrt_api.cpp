@@ -54,6 +54,7 @@ struct mrt_tracer {
     // fits the reference's stack in binary order could otherwise overflow in wide
     // order; sized this way no ray of the bound tree can overflow it.
     int wideStackCap = mrt::kStackCapacity;
+    int wideStackBound = mrt::kStackCapacity - 1;   // wide_stack_bound of the derived tree (the tail's headroom)
     double bindMs = 0.0;                   // wall time of the last bind / wide derivation (mrt_trace_info)
 
     // Launch scratch, one set per stream the handle has launched on: the stack
@@ -61,6 +62,7 @@ struct mrt_tracer {
     // running trace, so two traces in flight on different streams must not
     // share them (the handle's mutex only covers enqueueing).
     std::vector<mrt::Workspace*> workspaces;
+    uint64_t useClock = 0;   // launches of this handle (the workspaces' LRU order; guarded by mu)
     hipEvent_t evStart = nullptr, evStop = nullptr;
 
     // Occupancy per kernel variant (index variant_key(), below 256), queried once
@@ -358,7 +360,6 @@ int wait_all_workspaces(mrt_tracer* t) {
 // reached) the least recently used set once its last launch has completed —
 // grown to the grid's spill slab.
 int workspace_for(mrt_tracer* t, void* stream, int totalLanes, int ldsStack, int stackCap, mrt::Workspace** out) {
-    static uint64_t useClock = 0;
     mrt::Workspace* w = nullptr;
     for (mrt::Workspace* x : t->workspaces)
         if (x->stream == stream) w = x;
@@ -379,7 +380,7 @@ int workspace_for(mrt_tracer* t, void* stream, int totalLanes, int ldsStack, int
         MRT_HIP(hipEventCreateWithFlags(&w->done, mrt::kDoneEventFlags));
 #endif
     }
-    w->lastUse = ++useClock;
+    w->lastUse = ++t->useClock;
     const size_t need = (size_t)(stackCap - ldsStack) * (size_t)totalLanes;
     if (need > w->spillInts) {
         // A smaller slab may still be in use by this scratch's previous launch.
@@ -419,6 +420,7 @@ int refresh_wide(mrt_tracer* t) {
     t->wideBuiltFor = -1;
     t->wideFormat = mrt::kNodeCompact2;
     t->wideStackCap = mrt::kStackCapacity;
+    t->wideStackBound = mrt::kStackCapacity - 1;
     if (want) {
         std::vector<int32_t> host((size_t)(t->nodeBytes / 4));
         MRT_HIP(hipMemcpy(host.data(), t->nodes, (size_t)t->nodeBytes, hipMemcpyDeviceToHost));
@@ -444,6 +446,7 @@ int refresh_wide(mrt_tracer* t) {
             return MRT_OK;
         }
         t->wideStackCap = std::max<int>(mrt::kStackCapacity, (int)need + 1);
+        t->wideStackBound = (int)need;
         const int64_t bytes = (int64_t)wide.size() * 4;
         if (bytes > mrt::kMaxBufferBytes) return fail(MRT_ERR_TOO_LARGE, "4-wide node array above the 32-bit range");
         MRT_HIP(hipMalloc(&t->wideNodes, (size_t)bytes));
@@ -642,13 +645,16 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     a.woopBytes = (uint32_t)t->woopBytes;
     a.numRays = numRays;
     a.numQueues = cfg.num_queues < 0 ? 0 : std::min(cfg.num_queues, std::max(1, numRays));
-    a.fetchThreshold = cfg.fetch_threshold;
+    // the live-lane refill applies to the queue modes only (static rounds hand out one ray per
+    // lane per round, to every lane at once): a strided launch reports and uses 0
+    a.fetchThreshold = a.numQueues > 0 ? cfg.fetch_threshold : 0;
     a.specSlack = cfg.spec_slack;
     a.staticRounds = cfg.static_rounds;
     a.wideLeafCounts = wide && t->wideLeafCounts;
     a.laneGroupsLog2 = __builtin_ctz((unsigned)cfg.lane_groups);
     a.totalLanes = totalLanes;
     a.stackCap = stackCap;
+    a.stackBound = wide ? t->wideStackBound : stackCap - 1;
     a.tailLanes = cfg.tail_lanes;
     a.queues = ws->queues;
     a.spill = ws->spill;
@@ -692,9 +698,10 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
         MRT_HIP(hipMemcpy(&overflow, ws->status + mrt::kTimedSlot, sizeof(int), hipMemcpyDeviceToHost));
         info->stack_overflows = overflow;
         if (overflow)
-            return fail(MRT_ERR_STACK_OVERFLOW, std::to_string(overflow) +
-                                                    " stack pushes past the 64-entry traversal stack: those rays' "
-                                                    "results are incomplete (BVH deeper than the reference's STACK_SIZE)");
+            return fail(MRT_ERR_STACK_OVERFLOW,
+                        std::to_string(overflow) + " stack pushes past the " + std::to_string(stackCap) +
+                            "-entry traversal stack (stack_capacity): those rays' results are incomplete (BVH "
+                            "deeper than the reference's STACK_SIZE 64 allows in the binary order)");
     }
     return MRT_OK;
 }
@@ -881,6 +888,7 @@ int mrt_tracer_bind_info(const mrt_tracer* t, mrt_bind_info* info) {
     info->wide_bytes = t->wideNodes ? t->wideBytes : 0;
     info->wide_format = t->wideNodes ? t->wideFormat : mrt::kNodeCompact2;
     info->stack_capacity = t->wideNodes ? t->wideStackCap : mrt::kStackCapacity;
+    info->stack_bound = t->wideNodes ? t->wideStackBound : mrt::kStackCapacity - 1;
     return MRT_OK;
 }
 

@@ -43,11 +43,14 @@ struct TraceArgs {
     int laneGroupsLog2;        // strided mode: a wave's lanes take rays from 2^k spread-out sub-ranges
     int totalLanes;            // grid lanes (stride of the spill slab)
     int stackCap;              // stack entries incl. the sentinel (kStackCapacity, or the wide tree's bound)
-    int tailLanes;             // exact 4-wide speculative kernels: a wave that cannot refill and is down to
+    int stackBound;            // entries (sentinel excluded) a depth-first walk of the bound tree can hold
+                               // (wide_stack_bound; stackCap - 1 for the binary order): the frontier tail
+                               // keeps this much headroom before it expands more than one entry per step
+    int tailLanes;            // exact 4-wide speculative kernels: a wave that cannot refill and is down to
                                // this many live lanes finishes them in the frontier tail (0 = off)
     unsigned* queues;          // numQueues heads, kQueueStrideWords apart, zeroed per launch
     int* spill;                // (stackCap - S) * totalLanes ints
-    int* status;               // [0] = stack overflow count (lanes that pushed past kStackCapacity)
+    int* status;               // [0] = stack overflow count (entries pushed past stackCap)
     int4* stats;               // per-ray {nodes, tris, leaves, 0} (STATS variants)
 };
 

@@ -44,7 +44,8 @@ class TraceInfo(C.Structure):
 
 
 class BindInfo(C.Structure):
-    _fields_ = [("bind_ms", C.c_double), ("wide_bytes", i64), ("wide_format", i32), ("stack_capacity", i32)]
+    _fields_ = [("bind_ms", C.c_double), ("wide_bytes", i64), ("wide_format", i32), ("stack_capacity", i32),
+                ("stack_bound", i32)]
 
 
 class TunedSchedule(C.Structure):

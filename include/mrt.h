@@ -71,8 +71,9 @@ typedef struct mrt_launch_cfg {
                                   defaults, a batch over a BVH larger than the 256 MB Infinity Cache uses
                                   one global queue, refills at 48 live lanes, 12 waves/CU up to 3 rays per
                                   lane of a 16-wave grid, else 16 (mrt_trace_info reports what a launch used) */
-    int32_t fetch_threshold;   /* refill a wave when fewer than this many of its 64 lanes are live (0 = when all are done)
-                                  (reference DYNAMIC_FETCH_THRESHOLD 20 of 32, kepler_dynamic_fetch.cu:48) */
+    int32_t fetch_threshold;   /* queue modes (num_queues >= 1): refill a wave when fewer than this many of its
+                                  64 lanes are live (0 = when all are done; reference DYNAMIC_FETCH_THRESHOLD
+                                  20 of 32, kepler_dynamic_fetch.cu:48). Static strided rounds ignore it   */
     int32_t num_queues;        /* -1 (default) = static strided rounds, no atomics; 1..8 = the reference's
                                   dynamic fetch: a static first round, then one atomic per wave refill
                                   on the queue of the wave's XCD (xcc % num_queues), no stealing      */
@@ -120,8 +121,9 @@ typedef struct mrt_trace_info {
     int32_t lds_stack_entries; /* per-lane traversal-stack entries held in LDS                    */
     int32_t wide;              /* node width the launch traversed: 2 (Compact2) or 4              */
     int32_t num_queues;        /* ray queues the launch used (0 = static strided rounds)          */
-    int32_t fetch_threshold;   /* live-lane refill threshold the launch used                     */
-    int32_t stack_overflows;   /* pushes past the 64-entry stack in this launch (then the call returns
+    int32_t fetch_threshold;   /* live-lane refill threshold the launch used (0 for static strided rounds:
+                                  the refill applies to the queue modes only)                        */
+    int32_t stack_overflows;   /* entries pushed past stack_capacity in this launch (then the call returns
                                   MRT_ERR_STACK_OVERFLOW; 0 for any SBVH of depth <= 64)            */
     int32_t node_bytes;        /* bytes per node the launch read: 64 (Compact2 or quantized 4-wide), 128 */
     int32_t autotune_candidate; /* cfg.autotune: the schedule candidate this launch used (0..9), else -1 */
@@ -137,6 +139,10 @@ typedef struct mrt_bind_info {
     int64_t wide_bytes;        /* bytes of the derived 4-wide node array (0 = the Compact2 nodes)      */
     int32_t wide_format;       /* 0 = Compact2, 1 = exact 4-wide (128 B), 2 = quantized 4-wide (64 B)  */
     int32_t stack_capacity;    /* stack entries the wide traversal gets (see mrt_trace_info)          */
+    int32_t stack_bound;       /* entries (sentinel excluded) a depth-first walk of the bound tree can hold:
+                                  the wide tree's worst case (63 for the binary order). The frontier tail
+                                  expands several entries per step only while this much room stays free,
+                                  so it never needs more than stack_capacity either                     */
 } mrt_bind_info;
 
 /* One settled launch schedule of the autotuner (cfg.autotune): the candidate a batch
@@ -186,7 +192,7 @@ int  mrt_tracer_trace(mrt_tracer* t, const void* rays, void* results, int32_t nu
 /* Same, but blocking and event-timed around the launch only — the
  * reference's launch_tracingKernel contract (kepler_dynamic_fetch.cu:432-474).
  * Returns MRT_ERR_STACK_OVERFLOW (results written, info filled) when a ray of
- * this launch needed more than 64 stack entries. */
+ * this launch needed more than stack_capacity entries (64 in the binary order). */
 int  mrt_tracer_trace_timed(mrt_tracer* t, const void* rays, void* results, int32_t numRays,
                             uint32_t flags, int32_t* stats, void* stream, mrt_trace_info* info);
 

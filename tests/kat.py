@@ -163,3 +163,37 @@ def scene_comb(depth):
             child_box = ((0, 0, bottom), (1, 1, -(k + 1.0) + 0.5))
             b.set_inner(inner[k], child_box, leaf_box(k), inner[k + 1] * 4, tri_leaf(k))
     return b.buffers(), ray((0.25, 0.25, 1), (0, 0, -1), tmax=1000.0), (0, 2.0)
+
+
+def scene_complete(depth, hit_last=False):
+    """A complete binary tree of `depth` inner levels whose nested boxes
+    ([0,2]^2 x [0, 1 - level/64], so a level's boxes are larger than the next
+    level's) all hold (0.5, 0.5), one triangle per leaf (2^depth leaves): the
+    4-wide derivation collapses it level pair by level pair into a complete 4-ary
+    tree of depth/2 levels, every child of every node hit by a ray down -z through
+    (0.5, 0.5). Each leaf's
+    triangle is a small one in the corner (missed), except, with hit_last, the
+    last leaf's: a leg-2 triangle in the plane z = 0.5 (t = 1.5 from z = 2).
+    ADVICE r3: a frontier that expands many entries per step must still fit such a
+    ray's list in the stack. Returns (buffers, ray, (id, t))."""
+    b = Compact2Builder()
+    leaves = 1 << depth
+    counter = [0]
+
+    def leaf():
+        k = counter[0]
+        counter[0] += 1
+        z = 0.25 + 0.5 * (k % 2)
+        if hit_last and k == leaves - 1:
+            return b.leaf([(k, (0, 0, 0.5), (2, 0, 0.5), (0, 2, 0.5))])
+        return b.leaf([(k, (0, 0, z), (0.125, 0, z), (0, 0.125, z))])
+
+    def build(level):
+        idx = b.reserve_inner()
+        c = [build(level + 1) if level + 1 < depth else leaf() for _ in range(2)]
+        box = ((0, 0, 0), (2, 2, 1.0 - (level + 1) / 64.0))
+        return b.set_inner(idx, box, box, c[0], c[1])
+
+    build(0)
+    expect = (leaves - 1, 1.5) if hit_last else (-1, 1000.0)
+    return b.buffers(), ray((0.5, 0.5, 2), (0, 0, -1), tmax=1000.0), expect

@@ -268,6 +268,48 @@ def test_concurrent_streams_on_one_handle(tracer):
         tracer.set_config(**saved)
 
 
+def test_two_handles_from_two_host_threads():
+    """two tracer handles on one device, each with its own BVH, traced from
+    two host threads at once (the C calls release the GIL), blocking and asynchronous calls
+    interleaved on each thread's own stream, a set_config per round: every batch equals the
+    oracle — no cross-talk through the workspaces' LRU order or the waits."""
+    import threading
+    from mrt.tracer import GpuBvh, RayBuffer, Tracer
+    jobs = [scene_setup("bunny", 320, 240, "primary"), scene_setup("sponza", 256, 192, "diffuse")]
+    errors, outs = [], [[], []]
+
+    def worker(k):
+        try:
+            bufs, rays, any_hit, want, _ = jobs[k]
+            t = Tracer(0)
+            t.set_bvh(GpuBvh(bufs))
+            s = torch.cuda.Stream()
+            for rnd in range(6):
+                t.set_config(lds_stack=8 if rnd % 2 else 16)
+                rbs = [RayBuffer(rays, need_closest_hit=not any_hit) for _ in range(3)]
+                with torch.cuda.stream(s):
+                    t.trace_async(rbs[0], exact_rcp=True, stream=s)
+                    t.trace_batch(rbs[1], exact_rcp=True, stream=s)
+                    t.trace_async(rbs[2], exact_rcp=True, stream=s)
+                s.synchronize()
+                outs[k] += [rb.results_numpy()[:, :2] for rb in rbs]
+            assert t.last_info["stack_overflows"] == 0
+        except Exception as e:   # noqa: BLE001 — reported by the main thread
+            errors.append(e)
+
+    threads = [threading.Thread(target=worker, args=(k,)) for k in range(2)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=100)
+    assert not errors, errors
+    for k in range(2):
+        want = jobs[k][3]
+        assert len(outs[k]) == 18
+        for r in outs[k]:
+            assert np.array_equal(r, want[:, :2])
+
+
 @pytest.mark.parametrize("depth,overflow", [(40, False), (63, False), (64, True), (70, True)])
 def test_stack_overflow_is_reported(tracer, depth, overflow):
     """A comb BVH whose ray pushes one far leaf per level (kat.scene_comb): with 70
@@ -342,6 +384,39 @@ def test_frontier_tail_on_deep_stacks(tracer, depth, rays_n):
                 assert (res[:, 0] == expect[0]).all() and (res[:, 1] == kat.f2i(expect[1])).all()
             else:
                 assert (res[:, 0] >= 0).all()
+    finally:
+        tracer.set_config(**saved)
+
+
+@pytest.mark.parametrize("depth", [12, 14])
+@pytest.mark.parametrize("rays_n", [1, 3, 16, 17])
+def test_frontier_tail_on_wide_lists(tracer, depth, rays_n):
+    """a ray that hits every box of a complete 4-ary tree (kat.scene_complete)
+    makes the frontier tail's list grow by three per expanded node, past the depth-first
+    walk's worst case that sizes the stack. The tail keeps the tree's depth-first bound free
+    before a wide step (bind_info stack_bound), so no entry is pushed past stack_capacity:
+    no overflow, and the oracle's (and the hand) answer, closest and any hit, a miss and a
+    hit in the last leaf."""
+    from mrt.tracer import GpuBvh, RayBuffer
+    saved = tracer.config()
+    try:
+        tracer.set_config(wide=1, tail_lanes=16, autotune=0)
+        for hit_last in (False, True):
+            bufs, ray, expect = kat.scene_complete(depth, hit_last)
+            tracer.set_bvh(GpuBvh(bufs))
+            bi = tracer.bind_info()
+            assert bi["wide_format"] == 1 and bi["stack_bound"] == 3 * depth // 2
+            rays = np.stack([ray] * rays_n)
+            for closest in (True, False):
+                want, _, _ = O.trace(rays, *bufs, any_hit=not closest)
+                rb = RayBuffer(rays, need_closest_hit=closest)
+                rb.results.fill_(0x5A5A5A5A)
+                tracer.trace_batch(rb, exact_rcp=True)
+                res = rb.results_numpy()
+                assert tracer.last_info["stack_overflows"] == 0
+                assert (res[:, 2:] == 0x5A5A5A5A).all()
+                assert np.array_equal(res[:, :2], want[:, :2])
+                assert (res[:, 0] == expect[0]).all() and (res[:, 1] == kat.f2i(expect[1])).all()
     finally:
         tracer.set_config(**saved)
 

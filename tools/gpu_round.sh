@@ -1,17 +1,65 @@
 #!/bin/bash
-# One GPU-box session: parity tests, smoke, bench; every GPU step bounded.
-# GPU_ROUND_GLOO=1 also rehearses the N=2 sharded flow (two ranks on the one GPU, gloo collectives).
+# One GPU-box session as a list of steps, run in order; the first failing step ends the session
+# and every GPU step runs under a time limit of its own. Steps:
+#   test[=EXPR]     pytest -m gpu (with -k EXPR)                   -> gpurun_out/pytest_gpu.log
+#   smoke           __graft_entry__.smoke()                        -> gpurun_out/smoke.log
+#   bench[=ARGS]    bench.py ARGS (commas become spaces)           -> gpurun_out/bench.json, bench_detail.json
+#   gloo            the N=2 flow, two gloo ranks on the one GPU    -> gpurun_out/bench_gloo2.json
+#   tune            steady-state schedules of the bench workloads  -> gpurun_out/tuned_schedules.json
+#   profile=TAG     rocprofv3 kernel stats + PMC summaries of the bench workloads (PROF_WL overrides the list)
+#                                                                  -> gpurun_out/profiles/TAG_*
+#   readme          every README cell tuned, measured and checked  -> gpurun_out/readme_table.md
+#   timeline=W      per-ray start / tail entry / end of workload W (MRT_TAIL_TIMELINE variant library)
+# Usage: bash tools/gpu_round.sh test smoke bench      (gpurun -- 'bash tools/gpu_round.sh ...')
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
-mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
-tail -3 gpurun_out/pytest_gpu.log
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; tail -30 gpurun_out/smoke.log; exit 1; }
-tail -2 gpurun_out/smoke.log
-timeout -k 10 600 python bench.py ${BENCH_ARGS} > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -30 gpurun_out/bench.err; exit 1; }
-tail -c 600 gpurun_out/bench.json; grep -E "extra|head|strong" gpurun_out/bench.err
-if [ -n "$GPU_ROUND_GLOO" ]; then
-  timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
-    bench.py --gpus 2 --dist-backend gloo --steps 10 > gpurun_out/bench_gloo2.json 2> gpurun_out/bench_gloo2.err || { echo "gloo rehearsal failed"; tail -30 gpurun_out/bench_gloo2.err; exit 1; }
-  tail -c 1500 gpurun_out/bench_gloo2.json; grep -E "strong" gpurun_out/bench_gloo2.err
-fi
+mkdir -p gpurun_out; export TMPDIR=/tmp
+O=gpurun_out
+BENCH_WL="bunny-primary-1024x768 bunny-primary-640x480 conference-ao-640x480 sponza-diffuse-640x480 sponza-diffuse2-640x480 hairball-diffuse-640x480 hairball-diffuse-1920x1080"
+fail() { echo "$1 failed"; tail -30 "$2"; exit 1; }
+for step in "$@"; do
+  arg=""; [[ $step == *=* ]] && { arg=${step#*=}; step=${step%%=*}; }
+  case $step in
+    test)
+      K=(); [ -n "$arg" ] && K=(-k "$arg")
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider "${K[@]}" \
+        > $O/pytest_gpu.log 2>&1 || { grep -E "^(FAILED|ERROR)" $O/pytest_gpu.log | head; fail pytest $O/pytest_gpu.log; }
+      tail -1 $O/pytest_gpu.log ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || fail smoke $O/smoke.log
+      tail -1 $O/smoke.log ;;
+    bench)
+      timeout -k 10 600 python bench.py ${arg//,/ } --detail-out $O/bench_detail.json > $O/bench.json 2> $O/bench.err || fail bench $O/bench.err
+      grep -E "\[(head|extra|strong|line)\]" $O/bench.err ;;
+    gloo)
+      timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
+        bench.py --gpus 2 --dist-backend gloo --steps 10 --detail-out $O/bench_gloo2_detail.json > $O/bench_gloo2.json 2> $O/bench_gloo2.err \
+        || fail "gloo rehearsal" $O/bench_gloo2.err
+      grep -E "\[(head|strong)\]" $O/bench_gloo2.err ;;
+    tune)
+      rm -f $O/tuned_schedules.json
+      W=""; for w in $BENCH_WL; do [ $w = hairball-diffuse-1920x1080 ] || W="$W --workload $w"; done
+      timeout -k 10 900 python -u tools/tune_db.py $W --out $O/tuned_schedules.json > $O/tune_db.txt 2> $O/tune_db.err || fail tune_db $O/tune_db.err
+      timeout -k 10 300 python -u tools/tune_db.py --workload hairball-diffuse-1920x1080 --margin 0.015 --out $O/tuned_schedules.json \
+        >> $O/tune_db.txt 2>> $O/tune_db.err || fail "tune hairball" $O/tune_db.err
+      timeout -k 10 300 python -u tools/tune_db.py --workload bunny-primary-1024x768 --fast-rcp --out $O/tuned_schedules.json \
+        >> $O/tune_db.txt 2>> $O/tune_db.err || fail "tune fast" $O/tune_db.err
+      cut -c1-300 $O/tune_db.txt ;;
+    profile)
+      timeout -k 10 1150 bash tools/profile_all.sh ${arg:-round} ${PROF_WL:-$BENCH_WL fast:bunny-primary-1024x768} || exit 1
+      ls $O/profiles ;;
+    readme)
+      cp gpu-ray-tracing_amd/mrt/tuned_schedules.json $O/tuned_schedules_all.json
+      W=$(python3 -c "import sys; sys.path.insert(0,'tools'); import readme_table as r; print(' '.join('--workload '+c[0] for c in r.CELLS))")
+      timeout -k 10 900 python -u tools/tune_db.py $W --rounds 2 --launches 10 --out $O/tuned_schedules_all.json \
+        > $O/tune_db_readme.txt 2> $O/tune_db_readme.err || fail "tune readme" $O/tune_db_readme.err
+      timeout -k 10 900 python -u tools/readme_table.py --tune-db $O/tuned_schedules_all.json > $O/readme_table.log 2>&1 \
+        || fail "readme table" $O/readme_table.log
+      cat $O/readme_table.md ;;
+    timeline)
+      MRT_LIB_DIR=$PWD/gpu-ray-tracing_amd/lib/variants/tailtl timeout -k 10 300 python -u tools/tail_timeline.py $arg \
+        '{"tail_lanes": 0, "autotune": 0}' '{"tail_lanes": 16, "autotune": 0}' >> $O/tail_tl.txt 2>> $O/tail_tl.err || fail timeline $O/tail_tl.err
+      cut -c1-400 $O/tail_tl.txt ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
