@@ -39,7 +39,12 @@ def bench_line(log):
 
 
 line = bench_line(os.path.join(src, "bench_kt.log"))
-sched = line["detail"]["schedule"] if line else None
+sched = None
+if os.path.exists(os.path.join(src, "bench_kt_detail.json")):   # round 4+: the schedule is in the detail file
+    with open(os.path.join(src, "bench_kt_detail.json")) as f:
+        sched = json.load(f)["head"]["schedule"]
+elif line and "detail" in line:
+    sched = line["detail"]["schedule"]
 grid = sched["grid_waves"] * 64 if sched else None
 
 # the timed kernel = the trace_kernel instantiation with the most calls; its dispatches at the timed grid
