@@ -503,8 +503,11 @@ def cpu_baseline(batches, bufs, counted, threads, label, fast_results=None):
                 if fast is not None:
                     fr = fast_results[b]
                     fast["rays"] += len(rays)
-                    if any_hit:
-                        fast["any_hit_outcome_flips"] += int(((fr[:, 0] == -1) != (res[:, 0] == -1)).sum())
+                    if any_hit:   # hit/miss flips, classified edge / other like the closest-hit mismatches
+                        c = O.classify_any_hit_flips(rays, fr, res, woop, tri)
+                        fast["any_hit_outcome_flips"] += c["flips"]
+                        fast["edge"] += c["edge"]
+                        fast["other"] += c["other"]
                     else:
                         c = O.classify_fast_rcp(rays, fr, res, woop, tri)
                         for k in ("mismatch", "tie", "edge", "other"):

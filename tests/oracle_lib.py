@@ -144,6 +144,25 @@ def classify_fast_rcp(rays, gpu, want, woop, tri_index, limit=20000):
     return out
 
 
+def classify_any_hit_flips(rays, gpu, want, woop, tri_index):
+    """Any-hit rays whose hit/miss outcome differs between the fast-reciprocal GPU mode
+    and the oracle: an "edge" flip when the triangle that decided it (the GPU's hit, or
+    the oracle's) changes acceptance once 1/Dz moves by one ulp (v_rcp_f32's bound),
+    else "other". Returns {"flips", "edge", "other"}."""
+    rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)
+    woop = np.ascontiguousarray(woop).view(np.int32)
+    tri = np.ascontiguousarray(tri_index, np.int32)
+    live = woop.reshape(-1, 4)[:, 0] != np.int32(-2147483648)
+    flips = np.nonzero((gpu[:, 0] == -1) != (want[:, 0] == -1))[0]
+    out = {"flips": int(len(flips)), "edge": 0, "other": 0}
+    for i in flips:
+        tid = int(gpu[i, 0] if gpu[i, 0] != -1 else want[i, 0])
+        edge = any(len({woop_hit_rcp(rays[i], woop, s, float(rays[i][7]), k)[0] for k in (-1, 0, 1)}) > 1
+                   for s in np.nonzero((tri == tid) & live)[0])
+        out["edge" if edge else "other"] += 1
+    return out
+
+
 def brute_force(rays, woop, tri_index, any_hit=False):
     rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)
     woop = np.ascontiguousarray(woop).view(np.int32)

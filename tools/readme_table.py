@@ -4,8 +4,9 @@ the README's Kepler Mrays/s.
 
 Same measurement as bench.py (exact-rcp production kernel, device-generated
 rays, rays counted / kernel time of the timed steps); per cell also the
-oracle's agreement on the first `--parity-rays` rays of the batch (closest
-hit: id and t bit-identical; any hit: hit/miss identical). Scenes are the
+oracle's agreement on every ray of every batch of the cell (closest hit: id and
+t bit-identical; any hit: hit/miss identical; `--parity-rays N` checks a prefix
+of N rays per batch instead). Scenes are the
 deterministic stand-ins of csrc/host/scene.cpp; fairy, sibenik and san have no
 size in the README (their commonly distributed triangle counts are assumed).
 
@@ -50,7 +51,7 @@ def main():
     ap.add_argument("--bvh-cache", default="/tmp/mrt_bvhcache")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--parity-rays", type=int, default=16384)
+    ap.add_argument("--parity-rays", type=int, default=0, help="rays per batch checked against the oracle (0 = all)")
     ap.add_argument("--cells", default="", help="comma-separated subset of workloads")
     ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out"))
     ap.add_argument("--tune-db", default=None, help="saved schedules to lock (default: the package's)")
@@ -86,17 +87,20 @@ def main():
         wall, launch_ms, _ = bench.time_steps(launches, args.steps, args.warmup, 1)
         value = batches.rays_counted * args.steps / wall / 1e6
         kernel_ms = launch_ms * len(batches.batches)
-        # Parity on a prefix of the (first) batch against the oracle.
-        rb, _ = batches.batches[0]
-        n = min(args.parity_rays, rb.size)
-        rays = rb.rays.cpu().numpy()[:n]
-        gpu = rb.results_numpy()[:n]
-        any_hit = not rb.need_closest_hit
-        ref, _, _ = O.trace(rays, *bufs, any_hit=any_hit, threads=min(16, os.cpu_count() or 1))
-        if any_hit:
-            agree = float(((gpu[:, 0] == -1) == (ref[:, 0] == -1)).mean())
-        else:
-            agree = float(((gpu[:, 0] == ref[:, 0]) & (gpu[:, 1] == ref[:, 1])).mean())
+        # Parity of every ray of every batch (the timed launches' results) against the oracle.
+        n, same = 0, 0
+        for rb, _ in batches.batches:
+            k = rb.size if args.parity_rays <= 0 else min(args.parity_rays, rb.size)
+            rays = rb.rays.cpu().numpy()[:k]
+            gpu = rb.results_numpy()[:k]
+            any_hit = not rb.need_closest_hit
+            ref, _, _ = O.trace(rays, *bufs, any_hit=any_hit, threads=bench.host_threads())
+            if any_hit:
+                same += int(((gpu[:, 0] == -1) == (ref[:, 0] == -1)).sum())
+            else:
+                same += int(((gpu[:, 0] == ref[:, 0]) & (gpu[:, 1] == ref[:, 1])).sum())
+            n += k
+        agree = same / max(1, n)
         row = {
             "workload": name, "readme_mrays": readme, "readme_line": line,
             "mrays": round(value, 2), "x_readme": round(value / readme, 2),
@@ -106,7 +110,7 @@ def main():
             "per_ray": {"nodes": round(n_nodes / batches.rays_traced, 2), "tris": round(n_tris / batches.rays_traced, 2)},
             "alg_gbs": round(alg_bytes / (kernel_ms * 1e-3) / 1e9, 1),
             "schedule": bench.schedule_of(tracer, batches.batches[0][0], True)["name"],
-            "parity_rays": n, "parity_agree": agree, "parity_kind": "hit/miss" if any_hit else "id+t exact",
+            "parity_rays": n, "parity_all_rays": n == batches.rays_traced, "parity_agree": agree, "parity_kind": "hit/miss" if any_hit else "id+t exact",
         }
         rows.append(row)
         print(json.dumps(row), flush=True)
