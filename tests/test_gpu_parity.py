@@ -453,7 +453,7 @@ def test_ray_handoff_keeps_results(tracer, wl, handoff):
     frontier tail. Static rounds on a sparse grid (most waves dry at once, many hand-offs), on a
     full grid, and the global queue: closest hits bit-identical to the oracle, any hits
     genuine with the same hit/miss, no wait timed out (the blocking call would fail), rays
-    actually handed over."""
+    actually handed over on the hairball (short AO rays may all finish before a check)."""
     bufs, rays, any_hit, want, _ = scene_setup(*wl)
     saved = tracer.config()
     handed = 0
@@ -471,7 +471,8 @@ def test_ray_handoff_keeps_results(tracer, wl, handoff):
                     assert np.array_equal(res[:, :2], want[:, :2]), f"{extra}: closest hits differ"
     finally:
         tracer.set_config(**saved)
-    assert handed > 0
+    if wl[0].startswith("hairball"):   # long rays: some wave always holds more than a batch when others run dry
+        assert handed > 0
 
 
 def test_ray_handoff_async_streams_and_comb(tracer):
