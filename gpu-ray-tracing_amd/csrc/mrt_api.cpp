@@ -224,6 +224,7 @@ mrt_launch_cfg default_cfg() {
     c.autotune = kDefaultAutotune;
     c.tail_lanes = kDefaultTailLanes;
     c.handoff = kDefaultHandoff;
+    c.queue_shared = 0;
     return c;
 }
 
@@ -234,7 +235,8 @@ bool valid_cfg(const mrt_launch_cfg& c) {
            c.lane_groups >= 1 && c.lane_groups <= 64 && (c.lane_groups & (c.lane_groups - 1)) == 0 &&
            (c.wide >= 0 && c.wide <= 2) && c.spec_slack >= 0 && c.spec_slack <= 63 &&
            c.static_rounds >= 1 && c.static_rounds <= 64 && (c.autotune == 0 || c.autotune == 1) &&
-           c.tail_lanes >= 0 && c.tail_lanes <= 16 && c.handoff >= 0 && c.handoff <= 16;
+           c.tail_lanes >= 0 && c.tail_lanes <= 16 && c.handoff >= 0 && c.handoff <= 16 &&
+           c.queue_shared >= 0 && c.queue_shared <= 100;
 }
 
 // The frontier tail runs in the exact 4-wide kernels whose leaf refs carry counts.
@@ -385,8 +387,8 @@ int workspace_for(mrt_tracer* t, void* stream, int totalLanes, int ldsStack, int
         t->workspaces.push_back(w);
         // the queue heads, then one line of ray hand-off counters (zero between launches:
         // the last wave of a hand-off launch zeroes them)
-        MRT_HIP(hipMalloc(&w->queues, (mrt::kMaxQueues + 1) * mrt::kQueueStrideWords * sizeof(unsigned)));
-        MRT_HIP(hipMemset(w->queues, 0, (mrt::kMaxQueues + 1) * mrt::kQueueStrideWords * sizeof(unsigned)));
+        MRT_HIP(hipMalloc(&w->queues, (mrt::kHandoffLine + 1) * mrt::kQueueStrideWords * sizeof(unsigned)));
+        MRT_HIP(hipMemset(w->queues, 0, (mrt::kHandoffLine + 1) * mrt::kQueueStrideWords * sizeof(unsigned)));
         MRT_HIP(hipMalloc(&w->status, 64 * sizeof(int)));
         MRT_HIP(hipMemset(w->status, 0, 64 * sizeof(int)));
 #ifdef MRT_DONE_EVENT
@@ -668,6 +670,8 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     a.woopBytes = (uint32_t)t->woopBytes;
     a.numRays = numRays;
     a.numQueues = cfg.num_queues < 0 ? 0 : std::min(cfg.num_queues, std::max(1, numRays));
+    // queue_shared percent of the rays past the first round go to the shared queue
+    a.sharedRays = a.numQueues > 1 ? (int)((int64_t)numRays * cfg.queue_shared / 100) : 0;
     // the live-lane refill applies to the queue modes only (static rounds hand out one ray per
     // lane per round, to every lane at once): a strided launch reports and uses 0
     a.fetchThreshold = a.numQueues > 0 ? cfg.fetch_threshold : 0;
@@ -681,7 +685,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     a.tailLanes = cfg.tail_lanes;
     a.handoff = handoff;
     a.epoch = ++ws->epoch ? ws->epoch : ++ws->epoch;   // never 0 (a fresh record's flag)
-    a.handoffCtl = reinterpret_cast<int*>(ws->queues + mrt::kMaxQueues * mrt::kQueueStrideWords);
+    a.handoffCtl = reinterpret_cast<int*>(ws->queues + mrt::kHandoffLine * mrt::kQueueStrideWords);
     a.handoffRecs = ws->handoff;
     a.queues = ws->queues;
     a.spill = ws->spill;
@@ -693,7 +697,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     hipStream_t s = static_cast<hipStream_t>(stream);
     // Queue heads restart at zero for every launch; strided mode has none.
     if (a.numQueues > 0)
-        MRT_HIP(hipMemsetAsync(ws->queues, 0, mrt::kMaxQueues * mrt::kQueueStrideWords * sizeof(unsigned), s));
+        MRT_HIP(hipMemsetAsync(ws->queues, 0, mrt::kQueueLines * mrt::kQueueStrideWords * sizeof(unsigned), s));
     if (info) MRT_HIP(hipMemsetAsync(ws->status + mrt::kTimedSlot, 0, 4 * sizeof(int), s));
     if (info) MRT_HIP(hipEventRecord(t->evStart, s));
     if (slot) MRT_HIP(hipEventRecord(slot->start, s));

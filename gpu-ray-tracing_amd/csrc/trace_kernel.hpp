@@ -22,7 +22,10 @@ constexpr int kQueueStrideWords = 64;      // one 256-B line per queue head
 #define MRT_BLOCK_THREADS 256
 #endif
 constexpr int kBlockThreads = MRT_BLOCK_THREADS;   // wave64s per workgroup x 64 (default 4 waves)
-// Ray hand-off (trace_kernel.hip): counters of one launch, one 256-B line of their own.
+// Queue heads: kMaxQueues per-XCD heads, the shared queue's head (all zeroed per launch), then the
+// ray hand-off's counters (trace_kernel.hip), one 256-B line each.
+constexpr int kQueueLines = kMaxQueues + 1;
+constexpr int kHandoffLine = kQueueLines;
 enum : int { kHoReserve = 0, kHoTake = 1, kHoIdle = 2, kHoDry = 3, kHoExited = 4, kHoWords = 8 };
 constexpr int kHoRecordInt4 = 8;            // 128 B per exported ray
 constexpr int kStatusHandoffTimeouts = 2;   // Workspace::status words
@@ -41,6 +44,8 @@ struct TraceArgs {
     uint32_t woopBytes;
     int numRays;
     int numQueues;             // 1..8 ray queues (per-XCD heads)
+    int sharedRays;            // numQueues > 1: the batch's last rays in one queue every XCD's waves take
+                               // from once their own queue is dry (head kMaxQueues)
     int fetchThreshold;        // refill when fewer live lanes than this
     int specSlack;             // speculative: leave the node loop once <= this many lanes lack a leaf
     int staticRounds;          // queue modes: static strided rounds of the grid before the queues

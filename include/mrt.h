@@ -118,6 +118,9 @@ typedef struct mrt_launch_cfg {
                                   than this many rays hands the excess (as many as the idle waves asked for)
                                   over, whole state and stack, and each taker finishes up to this many at a
                                   time in the frontier tail (0..16; 0 = off; -1 = default)            */
+    int32_t queue_shared;      /* num_queues > 1: this percentage of the batch's rays (its end) goes to one
+                                  shared queue that a wave takes from once its XCD's queue is dry; the
+                                  rest is dealt in per-XCD contiguous shares (0..100; default 0)       */
 } mrt_launch_cfg;
 
 /* Per-launch statistics reported back to the host (optional). */

@@ -214,7 +214,11 @@ def test_exact_reciprocal_is_correctly_rounded_for_every_float(tracer):
                                  dict(tail_lanes=16, waves_per_cu=4), dict(tail_lanes=16, lds_stack=8),
                                  dict(tail_lanes=16, num_queues=1, fetch_threshold=48, waves_per_cu=4),
                                  dict(tail_lanes=12, num_queues=8, waves_per_cu=4, static_rounds=2),
-                                 dict(tail_lanes=16, num_queues=-1, fetch_threshold=16)],
+                                 dict(tail_lanes=16, num_queues=-1, fetch_threshold=16),
+                                 dict(num_queues=8, queue_shared=15, fetch_threshold=48, waves_per_cu=4),
+                                 dict(num_queues=8, queue_shared=100, waves_per_cu=4),
+                                 dict(num_queues=3, queue_shared=40, fetch_threshold=32, waves_per_cu=4, handoff=4),
+                                 dict(num_queues=8, queue_shared=15, fetch_threshold=48, waves_per_cu=20, handoff=16)],
                          ids=lambda c: ",".join(f"{k}={v}" for k, v in c.items()))
 def test_launch_configs_do_not_change_results(tracer, cfg):
     bufs, rays, any_hit, want, st = scene_setup("conference", 256, 192, "diffuse")

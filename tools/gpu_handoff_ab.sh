@@ -4,10 +4,12 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out; export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
-  -k "handoff or wide_lists or two_handles or frontier_tail or known_answers" > gpurun_out/pytest_ho.log 2>&1 || { grep -E "^(FAILED|ERROR)|Error" gpurun_out/pytest_ho.log | head -20; tail -30 gpurun_out/pytest_ho.log; exit 1; }
+  -k "handoff or wide_lists or two_handles or frontier_tail or known_answers or launch_configs" > gpurun_out/pytest_ho.log 2>&1 || { grep -E "^(FAILED|ERROR)|Error" gpurun_out/pytest_ho.log | head -20; tail -30 gpurun_out/pytest_ho.log; exit 1; }
 tail -1 gpurun_out/pytest_ho.log
 V=""
-for c in '{"autotune":0}' '{"autotune":0,"handoff":16}' '{"autotune":0,"handoff":8}' '{"autotune":0,"handoff":4}' '{"autotune":0,"handoff":2}'; do V="$V --variant lib:$c"; done
+for c in '{"autotune":0}' '{"autotune":0,"handoff":16}' '{"autotune":0,"handoff":8}' '{"autotune":0,"handoff":4}' '{"autotune":0,"handoff":2}' \
+         '{"autotune":0,"num_queues":8,"queue_shared":15,"fetch_threshold":48,"waves_per_cu":16}' \
+         '{"autotune":0,"num_queues":8,"queue_shared":15,"fetch_threshold":48,"waves_per_cu":16,"handoff":4}'; do V="$V --variant lib:$c"; done
 timeout -k 10 900 python -u tools/ab.py --rounds 5 --launches 20 --workload hairball-diffuse-640x480 --workload hairball-diffuse-1920x1080 \
   --workload mori-ao-640x480 --workload bunny-primary-1024x768 --workload bunny-primary-640x480 --workload conference-ao-640x480 \
   --workload sponza-diffuse-640x480 --variant 'lib/variants/r3:{"autotune":0}' $V > gpurun_out/ab_ho.txt 2> gpurun_out/ab_ho.err || { echo "ab failed"; tail -20 gpurun_out/ab_ho.err; exit 1; }
