@@ -12,5 +12,12 @@ for c in '{"autotune":0}' '{"autotune":0,"handoff":16}' '{"autotune":0,"handoff"
          '{"autotune":0,"num_queues":8,"queue_shared":15,"fetch_threshold":48,"waves_per_cu":16,"handoff":4}'; do V="$V --variant lib:$c"; done
 timeout -k 10 900 python -u tools/ab.py --rounds 5 --launches 20 --workload hairball-diffuse-640x480 --workload hairball-diffuse-1920x1080 \
   --workload mori-ao-640x480 --workload bunny-primary-1024x768 --workload bunny-primary-640x480 --workload conference-ao-640x480 \
-  --workload sponza-diffuse-640x480 --variant 'lib/variants/r3:{"autotune":0}' $V > gpurun_out/ab_ho.txt 2> gpurun_out/ab_ho.err || { echo "ab failed"; tail -20 gpurun_out/ab_ho.err; exit 1; }
+  --workload sponza-diffuse-640x480 --variant 'lib/variants/r3:{"autotune":0}' --variant 'lib/variants/doneev:{"autotune":0}' $V > gpurun_out/ab_ho.txt 2> gpurun_out/ab_ho.err || { echo "ab failed"; tail -20 gpurun_out/ab_ho.err; exit 1; }
 cat gpurun_out/ab_ho.txt
+timeout -k 10 900 bash tools/pmc_configs.sh hairball-diffuse-1920x1080 '{"autotune":0}' \
+  '{"autotune":0,"num_queues":1,"fetch_threshold":48,"waves_per_cu":20,"lane_groups":16}' \
+  '{"autotune":0,"num_queues":8,"queue_shared":15,"fetch_threshold":48,"waves_per_cu":16}' \
+  '{"autotune":0,"num_queues":8,"queue_shared":15,"fetch_threshold":48,"waves_per_cu":20}' \
+  '{"autotune":0,"num_queues":8,"queue_shared":30,"fetch_threshold":48,"waves_per_cu":16}' \
+  '{"autotune":0,"handoff":4}' > gpurun_out/pmc_cfg.txt 2>&1 || { echo "pmc failed"; tail gpurun_out/pmc_cfg.txt; exit 1; }
+cat gpurun_out/pmc_cfg.txt
