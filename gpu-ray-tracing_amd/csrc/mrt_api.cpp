@@ -125,9 +125,6 @@ struct Workspace {
                                   // (sticky); [kTimedSlot] = the current blocking launch's own count
     int* spill = nullptr;
     size_t spillInts = 0;
-    int4* handoff = nullptr;      // ray hand-off records (kHoRecordInt4 int4 per grid lane)
-    size_t handoffRecs = 0;
-    unsigned epoch = 0;           // launches on this scratch (the records' ready flag; never 0)
     // -DMRT_DONE_EVENT: recorded after every launch that uses this scratch, so waiting
     // for it never touches the stream (see workspace_wait)
     hipEvent_t done = nullptr;
@@ -205,11 +202,7 @@ constexpr int kTunedLaneGroups = 16;
 // What the autotuner's stage 2 tries when tail_lanes is left at its default (16: off).
 constexpr int kTunedTailLanes = 16;
 constexpr int kDefaultTailLanes = MRT_DEFAULT_TAIL_LANES;
-// The ray hand-off (trace_kernel.hip): rays a crowded wave hands to a dry one at a time.
-#ifndef MRT_DEFAULT_HANDOFF
-#define MRT_DEFAULT_HANDOFF 0
-#endif
-constexpr int kDefaultHandoff = MRT_DEFAULT_HANDOFF;
+
 
 mrt_launch_cfg default_cfg() {
     mrt_launch_cfg c;
@@ -223,8 +216,8 @@ mrt_launch_cfg default_cfg() {
     c.static_rounds = 1;
     c.autotune = kDefaultAutotune;
     c.tail_lanes = kDefaultTailLanes;
-    c.handoff = kDefaultHandoff;
     c.queue_shared = 0;
+    c.queue_block = 0;
     return c;
 }
 
@@ -235,8 +228,9 @@ bool valid_cfg(const mrt_launch_cfg& c) {
            c.lane_groups >= 1 && c.lane_groups <= 64 && (c.lane_groups & (c.lane_groups - 1)) == 0 &&
            (c.wide >= 0 && c.wide <= 2) && c.spec_slack >= 0 && c.spec_slack <= 63 &&
            c.static_rounds >= 1 && c.static_rounds <= 64 && (c.autotune == 0 || c.autotune == 1) &&
-           c.tail_lanes >= 0 && c.tail_lanes <= 16 && c.handoff >= 0 && c.handoff <= 16 &&
-           c.queue_shared >= 0 && c.queue_shared <= 100;
+           c.tail_lanes >= 0 && c.tail_lanes <= 16 &&
+           c.queue_shared >= 0 && c.queue_shared <= 100 && c.queue_block >= 0 && c.queue_block <= (1 << 20) &&
+           (c.queue_block & (c.queue_block - 1)) == 0 && (c.queue_block == 0 || c.queue_block >= 64);
 }
 
 // The frontier tail runs in the exact 4-wide kernels whose leaf refs carry counts.
@@ -370,8 +364,7 @@ int wait_all_workspaces(mrt_tracer* t) {
 // The scratch of `stream`: its own set, else a new one, else (kMaxWorkspaces
 // reached) the least recently used set once its last launch has completed —
 // grown to the grid's spill slab.
-int workspace_for(mrt_tracer* t, void* stream, int totalLanes, int ldsStack, int stackCap, bool handoff,
-                  mrt::Workspace** out) {
+int workspace_for(mrt_tracer* t, void* stream, int totalLanes, int ldsStack, int stackCap, mrt::Workspace** out) {
     mrt::Workspace* w = nullptr;
     for (mrt::Workspace* x : t->workspaces)
         if (x->stream == stream) w = x;
@@ -385,10 +378,7 @@ int workspace_for(mrt_tracer* t, void* stream, int totalLanes, int ldsStack, int
         w = new mrt::Workspace();
         w->stream = stream;
         t->workspaces.push_back(w);
-        // the queue heads, then one line of ray hand-off counters (zero between launches:
-        // the last wave of a hand-off launch zeroes them)
-        MRT_HIP(hipMalloc(&w->queues, (mrt::kHandoffLine + 1) * mrt::kQueueStrideWords * sizeof(unsigned)));
-        MRT_HIP(hipMemset(w->queues, 0, (mrt::kHandoffLine + 1) * mrt::kQueueStrideWords * sizeof(unsigned)));
+        MRT_HIP(hipMalloc(&w->queues, mrt::kQueueLines * mrt::kQueueStrideWords * sizeof(unsigned)));
         MRT_HIP(hipMalloc(&w->status, 64 * sizeof(int)));
         MRT_HIP(hipMemset(w->status, 0, 64 * sizeof(int)));
 #ifdef MRT_DONE_EVENT
@@ -406,15 +396,7 @@ int workspace_for(mrt_tracer* t, void* stream, int totalLanes, int ldsStack, int
         MRT_HIP(hipMalloc(&w->spill, need * sizeof(int)));
         w->spillInts = need;
     }
-    if (handoff && (size_t)totalLanes > w->handoffRecs) {
-        // every lane hands over at most one ray per launch (it takes no other afterwards)
-        if (int rc = workspace_wait(w)) return rc;
-        if (w->handoff) MRT_HIP(hipFree(w->handoff));
-        w->handoff = nullptr;
-        w->handoffRecs = 0;
-        MRT_HIP(hipMalloc(&w->handoff, (size_t)totalLanes * mrt::kHoRecordInt4 * sizeof(int4)));
-        w->handoffRecs = (size_t)totalLanes;
-    }
+
     if (!t->evStart) {
         // the blocking call's timing pair: no system-scope fence around the kernel (it would
         // flush the caches and be timed with it); the stop event releases to device scope,
@@ -657,8 +639,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     const bool wide = v.nodes != mrt::kNodeCompact2;
     const int stackCap = wide ? t->wideStackCap : mrt::kStackCapacity;
     mrt::Workspace* ws = nullptr;
-    const int handoff = v.tail && !v.stats ? cfg.handoff : 0;   // the tail kernels take rays from crowded waves
-    if (int rc = workspace_for(t, stream, totalLanes, v.ldsStack, stackCap, handoff > 0, &ws)) return rc;
+    if (int rc = workspace_for(t, stream, totalLanes, v.ldsStack, stackCap, &ws)) return rc;
 
     mrt::TraceArgs a{};
     a.rays = static_cast<const float4*>(rays);
@@ -672,6 +653,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     a.numQueues = cfg.num_queues < 0 ? 0 : std::min(cfg.num_queues, std::max(1, numRays));
     // queue_shared percent of the rays past the first round go to the shared queue
     a.sharedRays = a.numQueues > 1 ? (int)((int64_t)numRays * cfg.queue_shared / 100) : 0;
+    a.queueBlockLog2 = a.numQueues > 1 && cfg.queue_block > 0 ? __builtin_ctz((unsigned)cfg.queue_block) : 0;
     // the live-lane refill applies to the queue modes only (static rounds hand out one ray per
     // lane per round, to every lane at once): a strided launch reports and uses 0
     a.fetchThreshold = a.numQueues > 0 ? cfg.fetch_threshold : 0;
@@ -683,10 +665,6 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     a.stackCap = stackCap;
     a.stackBound = wide ? t->wideStackBound : stackCap - 1;
     a.tailLanes = cfg.tail_lanes;
-    a.handoff = handoff;
-    a.epoch = ++ws->epoch ? ws->epoch : ++ws->epoch;   // never 0 (a fresh record's flag)
-    a.handoffCtl = reinterpret_cast<int*>(ws->queues + mrt::kHandoffLine * mrt::kQueueStrideWords);
-    a.handoffRecs = ws->handoff;
     a.queues = ws->queues;
     a.spill = ws->spill;
     // The blocking call counts this launch's overflows in a slot of its own; the
@@ -698,7 +676,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     // Queue heads restart at zero for every launch; strided mode has none.
     if (a.numQueues > 0)
         MRT_HIP(hipMemsetAsync(ws->queues, 0, mrt::kQueueLines * mrt::kQueueStrideWords * sizeof(unsigned), s));
-    if (info) MRT_HIP(hipMemsetAsync(ws->status + mrt::kTimedSlot, 0, 4 * sizeof(int), s));
+    if (info) MRT_HIP(hipMemsetAsync(ws->status + mrt::kTimedSlot, 0, sizeof(int), s));
     if (info) MRT_HIP(hipEventRecord(t->evStart, s));
     if (slot) MRT_HIP(hipEventRecord(slot->start, s));
     MRT_HIP(mrt::launch_trace(v, a, blocks, s));
@@ -725,15 +703,9 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
         info->node_bytes = v.nodes == mrt::kNodeWide4 ? 128 : 64;
         info->num_queues = a.numQueues;
         info->fetch_threshold = a.fetchThreshold;
-        info->handoff = a.handoff;
-        int st[4] = {};
-        MRT_HIP(hipMemcpy(st, ws->status + mrt::kTimedSlot, sizeof(st), hipMemcpyDeviceToHost));
-        const int overflow = st[0];
-        info->handoff_rays = st[mrt::kStatusHandoffRays];
+        int overflow = 0;
+        MRT_HIP(hipMemcpy(&overflow, ws->status + mrt::kTimedSlot, sizeof(int), hipMemcpyDeviceToHost));
         info->stack_overflows = overflow;
-        if (st[mrt::kStatusHandoffTimeouts])
-            return fail(MRT_ERR_INTERNAL, std::to_string(st[mrt::kStatusHandoffTimeouts]) +
-                                              " waves gave up waiting in the ray hand-off: results may be incomplete");
         if (overflow)
             return fail(MRT_ERR_STACK_OVERFLOW,
                         std::to_string(overflow) + " stack pushes past the " + std::to_string(stackCap) +
@@ -789,7 +761,6 @@ const char* mrt_error_string(int err) {
         case MRT_ERR_NO_DEVICE: return "no HIP device";
         case MRT_ERR_TOO_LARGE: return "buffer or batch too large";
         case MRT_ERR_STACK_OVERFLOW: return "traversal stack overflow";
-        case MRT_ERR_INTERNAL: return "internal error";
         default: return "unknown error";
     }
 }
@@ -843,7 +814,6 @@ int mrt_tracer_destroy(mrt_tracer* t) {
             if (w->queues) (void)hipFree(w->queues);
             if (w->status) (void)hipFree(w->status);
             if (w->spill) (void)hipFree(w->spill);
-            if (w->handoff) (void)hipFree(w->handoff);
             delete w;
         }
         if (t->evStart) (void)hipEventDestroy(t->evStart);
@@ -902,7 +872,6 @@ int mrt_tracer_set_config(mrt_tracer* t, const mrt_launch_cfg* cfg) {
     if (c.static_rounds == 0) c.static_rounds = d.static_rounds;
     if (c.autotune < 0) c.autotune = d.autotune;
     if (c.tail_lanes < 0) c.tail_lanes = d.tail_lanes;
-    if (c.handoff < 0) c.handoff = d.handoff;
     if (!valid_cfg(c)) return fail(MRT_ERR_INVALID_ARG, "launch config out of range");
     std::lock_guard<std::mutex> lock(t->mu);
     t->cfg = c;

@@ -22,14 +22,9 @@ constexpr int kQueueStrideWords = 64;      // one 256-B line per queue head
 #define MRT_BLOCK_THREADS 256
 #endif
 constexpr int kBlockThreads = MRT_BLOCK_THREADS;   // wave64s per workgroup x 64 (default 4 waves)
-// Queue heads: kMaxQueues per-XCD heads, the shared queue's head (all zeroed per launch), then the
-// ray hand-off's counters (trace_kernel.hip), one 256-B line each.
+// Queue heads: kMaxQueues per-XCD heads and the shared queue's head, one 256-B line each,
+// zeroed per launch.
 constexpr int kQueueLines = kMaxQueues + 1;
-constexpr int kHandoffLine = kQueueLines;
-enum : int { kHoReserve = 0, kHoTake = 1, kHoIdle = 2, kHoDry = 3, kHoExited = 4, kHoWords = 8 };
-constexpr int kHoRecordInt4 = 8;            // 128 B per exported ray
-constexpr int kStatusHandoffTimeouts = 2;   // Workspace::status words
-constexpr int kStatusHandoffRays = 3;
 // Largest node / woop buffer a tracer binds (32-bit buffer offsets).
 constexpr int64_t kMaxBufferBytes = 0xFFFFFFC0ll;
 
@@ -46,6 +41,7 @@ struct TraceArgs {
     int numQueues;             // 1..8 ray queues (per-XCD heads)
     int sharedRays;            // numQueues > 1: the batch's last rays in one queue every XCD's waves take
                                // from once their own queue is dry (head kMaxQueues)
+    int queueBlockLog2;        // numQueues > 1: 0 = contiguous shares, k = 2^k-ray blocks dealt cyclically
     int fetchThreshold;        // refill when fewer live lanes than this
     int specSlack;             // speculative: leave the node loop once <= this many lanes lack a leaf
     int staticRounds;          // queue modes: static strided rounds of the grid before the queues
@@ -58,15 +54,9 @@ struct TraceArgs {
                                // keeps this much headroom before it expands more than one entry per step
     int tailLanes;            // exact 4-wide speculative kernels: a wave that cannot refill and is down to
                                // this many live lanes finishes them in the frontier tail (0 = off)
-    int handoff;               // exact 4-wide tail kernels: rays a crowded wave hands to dry waves at a time
-                               // (0 = off); see trace_kernel.hip "ray hand-off"
-    unsigned epoch;            // launch number on this workspace (nonzero): the hand-off records' ready flag
-    int* handoffCtl;           // kHoWords counters (kHoReserve ...); zero at launch, reset by the last wave out
-    int4* handoffRecs;         // totalLanes records of kHoRecordInt4 int4 (one 128-B line each)
     unsigned* queues;          // numQueues heads, kQueueStrideWords apart, zeroed per launch
     int* spill;                // (stackCap - S) * totalLanes ints
-    int* status;               // [0] = stack overflow count (entries pushed past stackCap);
-                               // [kStatusHandoffTimeouts] = hand-off waits that gave up (sticky)
+    int* status;               // [0] = stack overflow count (entries pushed past stackCap)
     int4* stats;               // per-ray {nodes, tris, leaves, 0} (STATS variants)
 };
 

@@ -45,10 +45,8 @@ enum {
     MRT_ERR_HIP = 3,           /* a HIP runtime call failed                  */
     MRT_ERR_NO_DEVICE = 4,     /* no GPU visible                             */
     MRT_ERR_TOO_LARGE = 5,     /* buffer beyond the 4 GiB buffer-offset range, or > 2^30 rays per launch */
-    MRT_ERR_STACK_OVERFLOW = 6,/* a ray needed more than the reference's 64 stack entries
+    MRT_ERR_STACK_OVERFLOW = 6 /* a ray needed more than the reference's 64 stack entries
                                   (kepler_dynamic_fetch.cu:47 STACK_SIZE): its result is incomplete */
-    MRT_ERR_INTERNAL = 7       /* a bounded wait inside the kernel gave up (ray hand-off): results may be
-                                  incomplete; never expected                                           */
 };
 
 /* ---- trace flags (bit set) -------------------------------------------- */
@@ -113,14 +111,12 @@ typedef struct mrt_launch_cfg {
                                   rays (at least four), up to 16/R pending nodes or four-triangle leaf chunks
                                   per ray per memory round trip, regrouping as rays finish (0..16; 0 = off;
                                   default 16; -1 = default; the autotuner tries 0 when left at the default) */
-    int32_t handoff;           /* ray hand-off (with the frontier tail): a wave that has run dry waits for rays
-                                  instead of leaving; a wave that can no longer refill and still holds more
-                                  than this many rays hands the excess (as many as the idle waves asked for)
-                                  over, whole state and stack, and each taker finishes up to this many at a
-                                  time in the frontier tail (0..16; 0 = off; -1 = default)            */
     int32_t queue_shared;      /* num_queues > 1: this percentage of the batch's rays (its end) goes to one
                                   shared queue that a wave takes from once its XCD's queue is dry; the
                                   rest is dealt in per-XCD contiguous shares (0..100; default 0)       */
+    int32_t queue_block;       /* num_queues > 1: 0 = each queue's share is contiguous; a power of two >= 64 =
+                                  the shares are this many rays' blocks dealt cyclically (block i to queue
+                                  i mod num_queues), so every XCD samples the whole frame              */
 } mrt_launch_cfg;
 
 /* Per-launch statistics reported back to the host (optional). */
@@ -141,8 +137,6 @@ typedef struct mrt_trace_info {
     int32_t stack_capacity;    /* stack entries (sentinel included) the launch had: 64 = the reference's
                                   for the binary order; the wide orders get the bound tree's worst case
                                   (never less than 64), so no ray of a tree overflows there          */
-    int32_t handoff;           /* the ray hand-off batch the launch used (0 = off)                     */
-    int32_t handoff_rays;      /* rays this launch handed from crowded waves to dry ones               */
 } mrt_trace_info;
 
 /* What the last bind derived (mrt_tracer_bind_info). */

@@ -217,8 +217,11 @@ def test_exact_reciprocal_is_correctly_rounded_for_every_float(tracer):
                                  dict(tail_lanes=16, num_queues=-1, fetch_threshold=16),
                                  dict(num_queues=8, queue_shared=15, fetch_threshold=48, waves_per_cu=4),
                                  dict(num_queues=8, queue_shared=100, waves_per_cu=4),
-                                 dict(num_queues=3, queue_shared=40, fetch_threshold=32, waves_per_cu=4, handoff=4),
-                                 dict(num_queues=8, queue_shared=15, fetch_threshold=48, waves_per_cu=20, handoff=16)],
+                                 dict(num_queues=3, queue_shared=40, fetch_threshold=32, waves_per_cu=4),
+                                 dict(num_queues=8, queue_shared=15, fetch_threshold=48, waves_per_cu=20),
+                                 dict(num_queues=8, queue_shared=10, queue_block=4096, fetch_threshold=48, waves_per_cu=4),
+                                 dict(num_queues=8, queue_block=64, waves_per_cu=4),
+                                 dict(num_queues=5, queue_shared=5, queue_block=1024, fetch_threshold=40, waves_per_cu=4)],
                          ids=lambda c: ",".join(f"{k}={v}" for k, v in c.items()))
 def test_launch_configs_do_not_change_results(tracer, cfg):
     bufs, rays, any_hit, want, st = scene_setup("conference", 256, 192, "diffuse")
@@ -443,71 +446,6 @@ def test_tail_lanes_keep_results(tracer, wl, tail):
         assert_valid_hits(rays, res, want, bufs)
     else:
         assert np.array_equal(res[:, :2], want[:, :2])
-
-
-HANDOFF_WL = [("hairball:800", 256, 192, "diffuse"), ("bunny", 320, 240, "primary"), ("mori", 256, 192, "ao"),
-              ("sibenik", 256, 192, "diffuse"), ("conference", 256, 192, "ao")]
-
-
-@pytest.mark.parametrize("wl", HANDOFF_WL, ids=lambda w: "-".join(map(str, w)))
-@pytest.mark.parametrize("handoff", [1, 4, 16])
-def test_ray_handoff_keeps_results(tracer, wl, handoff):
-    """The ray hand-off (cfg.handoff): waves that ran dry wait for rays, a wave that can no
-    longer refill hands rays over (whole state and stack) and the taker finishes them in the
-    frontier tail. Static rounds on a sparse grid (most waves dry at once, many hand-offs), on a
-    full grid, and the global queue: closest hits bit-identical to the oracle, any hits
-    genuine with the same hit/miss, no wait timed out (the blocking call would fail), rays
-    actually handed over on the hairball (short AO rays may all finish before a check)."""
-    bufs, rays, any_hit, want, _ = scene_setup(*wl)
-    saved = tracer.config()
-    handed = 0
-    try:
-        for extra in ({"waves_per_cu": 4}, {"waves_per_cu": 20}, {"num_queues": 1, "fetch_threshold": 48, "waves_per_cu": 8}):
-            tracer.set_config(**{**saved, "tail_lanes": 16, "handoff": handoff, "autotune": 0, **extra})
-            for _ in range(2):   # a second launch on the same scratch: the counters were left at zero
-                res, _ = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=True)
-                info = tracer.last_info
-                assert info["handoff"] == handoff and info["stack_overflows"] == 0
-                handed += info["handoff_rays"]
-                if any_hit:
-                    assert_valid_hits(rays, res, want, bufs)
-                else:
-                    assert np.array_equal(res[:, :2], want[:, :2]), f"{extra}: closest hits differ"
-    finally:
-        tracer.set_config(**saved)
-    if wl[0].startswith("hairball"):   # long rays: some wave always holds more than a batch when others run dry
-        assert handed > 0
-
-
-def test_ray_handoff_async_streams_and_comb(tracer):
-    """Hand-off launches back to back on two streams (each stream its own counters and
-    records, each launch its own ready flags), on the comb scene whose deep rays keep their
-    stacks in the spill slab (not handed over) next to shallow ones: every batch exact."""
-    from mrt.tracer import GpuBvh, RayBuffer
-    bufs, rays, _, want, _ = scene_setup("hairball:800", 256, 192, "diffuse")
-    saved = tracer.config()
-    try:
-        tracer.set_config(tail_lanes=16, handoff=4, autotune=0, waves_per_cu=8)
-        tracer.set_bvh(GpuBvh(bufs))
-        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
-        rbs = [RayBuffer(rays, need_closest_hit=True) for _ in range(6)]
-        torch.cuda.synchronize()
-        for k, rb in enumerate(rbs):
-            s = s1 if k % 2 == 0 else s2
-            with torch.cuda.stream(s):
-                tracer.trace_async(rb, exact_rcp=True, stream=s)
-        s1.synchronize()
-        s2.synchronize()
-        for rb in rbs:
-            assert np.array_equal(rb.results_numpy()[:, :2], want[:, :2])
-        cb, ray, expect = kat.scene_comb(40)
-        tracer.set_bvh(GpuBvh(cb))
-        rb = RayBuffer(np.stack([ray] * 3000), need_closest_hit=True)
-        tracer.trace_batch(rb, exact_rcp=True)
-        res = rb.results_numpy()
-        assert (res[:, 0] == expect[0]).all() and (res[:, 1] == kat.f2i(expect[1])).all()
-    finally:
-        tracer.set_config(**saved)
 
 
 def fuzz_rays(scene, n, seed, w=96, h=72):
