@@ -15,7 +15,7 @@ for c in '{"autotune":0}' \
          '{"autotune":0,"num_queues":8,"queue_shared":30,"fetch_threshold":48,"waves_per_cu":16}'; do V="$V --variant lib:$c"; done
 timeout -k 10 900 python -u tools/ab.py --rounds 5 --launches 20 --workload hairball-diffuse-1920x1080 --workload hairball-diffuse-640x480 \
   --workload bunny-primary-1024x768 --workload bunny-primary-640x480 --workload mori-ao-640x480 --workload conference-ao-640x480 \
-  --workload sponza-diffuse-640x480 --variant 'lib/variants/r3:{"autotune":0}' --variant 'lib/variants/c1:{"autotune":0}' $V > gpurun_out/ab_q.txt 2> gpurun_out/ab_q.err || { echo "ab failed"; tail -20 gpurun_out/ab_q.err; exit 1; }
+  --workload sponza-diffuse-640x480 --variant 'lib/variants/r3:{"autotune":0}' --variant 'lib/variants/c1:{"autotune":0}' --variant 'lib/variants/noshares:{"autotune":0}' --variant 'lib/variants/nolate:{"autotune":0}' --variant 'lib/variants/noboth:{"autotune":0}' $V > gpurun_out/ab_q.txt 2> gpurun_out/ab_q.err || { echo "ab failed"; tail -20 gpurun_out/ab_q.err; exit 1; }
 cat gpurun_out/ab_q.txt
 timeout -k 10 900 bash tools/pmc_configs.sh hairball-diffuse-1920x1080 '{"autotune":0}' \
   '{"autotune":0,"num_queues":8,"queue_shared":10,"queue_block":4096,"fetch_threshold":48,"waves_per_cu":16}' \
