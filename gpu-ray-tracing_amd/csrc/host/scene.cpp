@@ -520,10 +520,15 @@ void gen_san(Scene& sc, uint64_t seed) {   // 10 500 000 triangles: courtyard, a
 
 // param > 0: a smaller ball of that many tubes (same density of strands per
 // tube, no padding strip), e.g. for GPU tests of the deep, incoherent case.
+// Hairball: 14 975 random-walk tubes of 36 segments, 6 sides (round 4; round 3 had 29 950 tubes of 18
+// twice-as-long segments). Shorter, less sliver-like segments keep the SBVH's spatial splits rare: the
+// full scene's SBVH has 1.52 M inner nodes and 1.13 references per triangle against the README's
+// 1 249 052 inner nodes for the real asset (README.md:54); the round-3 stand-in had 2.32 M and 1.92.
 void gen_hairball(Scene& sc, uint64_t seed, int64_t param) {   // 6 469 561 triangles
     Mesher m(sc);
     Rng rng(seed);
-    const int tubes = param > 0 ? (int)std::min<int64_t>(param, 29950) : 29950, segments = 18, sides = 6;
+    const int segments = 36, sides = 6, fullTubes = 6469561 / (segments * sides * 2);
+    const int tubes = param > 0 ? (int)std::min<int64_t>(param, fullTubes) : fullTubes;
     sc.vertices.reserve((size_t)tubes * (segments + 1) * sides + 4096);
     sc.triangles.reserve(6469561);
     std::vector<std::array<double, 3>> pts(segments + 1);
@@ -541,7 +546,7 @@ void gen_hairball(Scene& sc, uint64_t seed, int64_t param) {   // 6 469 561 tria
             if (r2 > 0.8)
                 for (int c = 0; c < 3; c++) d[c] -= 0.6 * p[c];
             const double dl = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]) + 1e-12;
-            for (int c = 0; c < 3; c++) p[c] += 0.035 * d[c] / dl;
+            for (int c = 0; c < 3; c++) p[c] += 0.0175 * d[c] / dl;
         }
         m.tube(pts, 0.0035, sides);
     }
