@@ -67,7 +67,7 @@ struct mrt_tracer {
 
     // Occupancy per kernel variant (index variant_key(), below 256), queried once
     // (hipOccupancy* is a host round-trip that would otherwise sit on every launch).
-    int occ[1024] = {};
+    int occ[512] = {};
 
     // cfg.autotune: per (batch size, variant) the ray-distribution schedule the
     // measured launches chose (mrt_api.cpp autotune_*), reset on bind/set_config.
@@ -202,11 +202,7 @@ constexpr int kTunedLaneGroups = 16;
 // What the autotuner's stage 2 tries when tail_lanes is left at its default (16: off).
 constexpr int kTunedTailLanes = 16;
 constexpr int kDefaultTailLanes = MRT_DEFAULT_TAIL_LANES;
-// The workgroup hand-off (trace_kernel.hip): rays a crowded wave keeps (0 = off).
-#ifndef MRT_DEFAULT_HANDOFF
-#define MRT_DEFAULT_HANDOFF 0
-#endif
-constexpr int kDefaultHandoff = MRT_DEFAULT_HANDOFF;
+
 
 
 mrt_launch_cfg default_cfg() {
@@ -223,7 +219,6 @@ mrt_launch_cfg default_cfg() {
     c.tail_lanes = kDefaultTailLanes;
     c.queue_shared = 0;
     c.queue_block = 0;
-    c.handoff = kDefaultHandoff;
     return c;
 }
 
@@ -236,8 +231,7 @@ bool valid_cfg(const mrt_launch_cfg& c) {
            c.static_rounds >= 1 && c.static_rounds <= 64 && (c.autotune == 0 || c.autotune == 1) &&
            c.tail_lanes >= 0 && c.tail_lanes <= 16 &&
            c.queue_shared >= 0 && c.queue_shared <= 100 && c.queue_block >= 0 && c.queue_block <= (1 << 20) &&
-           (c.queue_block & (c.queue_block - 1)) == 0 && (c.queue_block == 0 || c.queue_block >= 64) &&
-           c.handoff >= 0 && c.handoff <= 16;
+           (c.queue_block & (c.queue_block - 1)) == 0 && (c.queue_block == 0 || c.queue_block >= 64);
 }
 
 // The frontier tail runs in the exact 4-wide kernels whose leaf refs carry counts.
@@ -256,7 +250,6 @@ mrt::TraceVariant variant_for(const mrt_tracer* t, uint32_t flags) {
     // the Compact2 nodes, and with them the oracle's exact per-ray counters.
     v.nodes = (t->cfg.wide != 0 && t->wideNodes != nullptr && v.speculative) ? t->wideFormat : mrt::kNodeCompact2;
     v.tail = with_tail(t, v, t->cfg);
-    v.handoff = v.tail && !v.stats && t->cfg.handoff > 0;
     return v;
 }
 
@@ -280,10 +273,10 @@ constexpr int kAutoMinWaves = 8;
 // workgroup is resident at once.
 int variant_key(const mrt::TraceVariant& v) {
     const int lds = v.ldsStack == 8 ? 0 : v.ldsStack == 16 ? 1 : 2;
-    static_assert((15 | (2 << 4) | (mrt::kNodeWide4Q << 6) | (1 << 8) | (1 << 9)) < (int)(sizeof(mrt_tracer::occ) / sizeof(int)),
+    static_assert((15 | (2 << 4) | (mrt::kNodeWide4Q << 6) | (1 << 8)) < (int)(sizeof(mrt_tracer::occ) / sizeof(int)),
                   "every variant_key indexes mrt_tracer::occ");
     return (v.anyHit ? 1 : 0) | (v.speculative ? 2 : 0) | (v.exactRcp ? 4 : 0) | (v.stats ? 8 : 0) | (lds << 4) |
-           (v.nodes << 6) | (v.tail ? 256 : 0) | (v.handoff ? 512 : 0);   // < 1024 = the size of mrt_tracer::occ
+           (v.nodes << 6) | (v.tail ? 256 : 0);   // < 512 = the size of mrt_tracer::occ
 }
 
 // The launch configuration a trace uses: the tracer's, except that with every
@@ -642,7 +635,6 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
         cfg = tune_candidate(cfg, cand, tune->stage1);
     }
     v.tail = with_tail(t, v, cfg);   // a tuned candidate may run without the tail
-    v.handoff = v.tail && !v.stats && cfg.handoff > 0;
     const int blocks = grid_blocks(t, cfg, v, numRays, &perCU);
     const int totalLanes = blocks * mrt::kBlockThreads;
     const bool wide = v.nodes != mrt::kNodeCompact2;
@@ -674,7 +666,6 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     a.stackCap = stackCap;
     a.stackBound = wide ? t->wideStackBound : stackCap - 1;
     a.tailLanes = cfg.tail_lanes;
-    a.handoff = v.handoff ? cfg.handoff : 0;
     a.queues = ws->queues;
     a.spill = ws->spill;
     // The blocking call counts this launch's overflows in a slot of its own; the
@@ -713,7 +704,6 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
         info->node_bytes = v.nodes == mrt::kNodeWide4 ? 128 : 64;
         info->num_queues = a.numQueues;
         info->fetch_threshold = a.fetchThreshold;
-        info->handoff = a.handoff;
         int overflow = 0;
         MRT_HIP(hipMemcpy(&overflow, ws->status + mrt::kTimedSlot, sizeof(int), hipMemcpyDeviceToHost));
         info->stack_overflows = overflow;
@@ -883,7 +873,6 @@ int mrt_tracer_set_config(mrt_tracer* t, const mrt_launch_cfg* cfg) {
     if (c.static_rounds == 0) c.static_rounds = d.static_rounds;
     if (c.autotune < 0) c.autotune = d.autotune;
     if (c.tail_lanes < 0) c.tail_lanes = d.tail_lanes;
-    if (c.handoff < 0) c.handoff = d.handoff;
     if (!valid_cfg(c)) return fail(MRT_ERR_INVALID_ARG, "launch config out of range");
     std::lock_guard<std::mutex> lock(t->mu);
     t->cfg = c;

@@ -22,11 +22,6 @@ constexpr int kQueueStrideWords = 64;      // one 256-B line per queue head
 #define MRT_BLOCK_THREADS 256
 #endif
 constexpr int kBlockThreads = MRT_BLOCK_THREADS;   // wave64s per workgroup x 64 (default 4 waves)
-// Workgroup hand-off mailbox (LDS): header words, then kHoRays records of kHoRecordInts ints.
-enum : int { kHoIdleMask = 0, kHoState = 1, kHoDry = 2, kHoHeader = 4 };
-constexpr int kHoRays = 16;
-constexpr int kHoRecordInts = 32;       // 13 state words, 3 spare, 16 stack entries
-constexpr int kHoMaxPolls = 1 << 22;
 // Queue heads: kMaxQueues per-XCD heads and the shared queue's head, one 256-B line each,
 // zeroed per launch.
 constexpr int kQueueLines = kMaxQueues + 1;
@@ -57,9 +52,7 @@ struct TraceArgs {
     int stackBound;            // entries (sentinel excluded) a depth-first walk of the bound tree can hold
                                // (wide_stack_bound; stackCap - 1 for the binary order): the frontier tail
                                // keeps this much headroom before it expands more than one entry per step
-    int tailLanes;
-    int handoff;               // HO kernels: a wave that cannot refill keeps this many rays and hands the rest
-                               // to idle waves of its workgroup (trace_kernel.hip "workgroup hand-off")            // exact 4-wide speculative kernels: a wave that cannot refill and is down to
+    int tailLanes;            // exact 4-wide speculative kernels: a wave that cannot refill and is down to
                                // this many live lanes finishes them in the frontier tail (0 = off)
     unsigned* queues;          // numQueues heads, kQueueStrideWords apart, zeroed per launch
     int* spill;                // (stackCap - S) * totalLanes ints
@@ -80,7 +73,6 @@ struct TraceVariant {
     int ldsStack;       // 8, 16 or 32 LDS entries per lane
     int nodes = 0;      // kNodeCompact2, or a 4-wide form derived from it (speculative mode only)
     bool tail = false;  // kNodeWide4 with leaf counts: the instantiation with the frontier tail
-    bool handoff = false;   // tail + the workgroup hand-off (trace_kernel.hip)
 };
 
 // The 4-wide node array derived from a Compact2 node array (numNodes inner nodes,

@@ -117,11 +117,6 @@ typedef struct mrt_launch_cfg {
     int32_t queue_block;       /* num_queues > 1: 0 = each queue's share is contiguous; a power of two >= 64 =
                                   the shares are this many rays' blocks dealt cyclically (block i to queue
                                   i mod num_queues), so every XCD samples the whole frame              */
-    int32_t handoff;           /* workgroup hand-off (with the frontier tail): a wave that has run dry waits
-                                  (in LDS) for rays of its workgroup; a wave that can no longer refill and
-                                  holds more than this many rays hands up to 16 at a time, whole state and
-                                  stack, to an idle wave of its workgroup, which finishes them in the
-                                  frontier tail (0..16; 0 = off, default; -1 = default)               */
 } mrt_launch_cfg;
 
 /* Per-launch statistics reported back to the host (optional). */
@@ -142,7 +137,6 @@ typedef struct mrt_trace_info {
     int32_t stack_capacity;    /* stack entries (sentinel included) the launch had: 64 = the reference's
                                   for the binary order; the wide orders get the bound tree's worst case
                                   (never less than 64), so no ray of a tree overflows there          */
-    int32_t handoff;           /* the workgroup hand-off the launch used (cfg.handoff; 0 = off)        */
 } mrt_trace_info;
 
 /* What the last bind derived (mrt_tracer_bind_info). */

@@ -448,67 +448,6 @@ def test_tail_lanes_keep_results(tracer, wl, tail):
         assert np.array_equal(res[:, :2], want[:, :2])
 
 
-HANDOFF_WL = [("hairball:800", 256, 192, "diffuse"), ("bunny", 320, 240, "primary"), ("mori", 256, 192, "ao"),
-              ("sibenik", 256, 192, "diffuse"), ("conference", 256, 192, "ao")]
-
-
-@pytest.mark.parametrize("wl", HANDOFF_WL, ids=lambda w: "-".join(map(str, w)))
-@pytest.mark.parametrize("handoff", [1, 4, 16])
-def test_workgroup_handoff_keeps_results(tracer, wl, handoff):
-    """The workgroup hand-off (cfg.handoff): a dry wave waits in LDS for rays of its
-    workgroup; a wave that can no longer refill hands rays over (whole state and stack)
-    through the workgroup's mailbox and the taker finishes them in the frontier tail. Static
-    rounds on a sparse grid, on a full grid, and the global queue, twice each on the same
-    scratch: closest hits bit-identical to the oracle, any hits genuine with the same hit/miss,
-    no bounded wait gave up (it would count as a stack overflow)."""
-    bufs, rays, any_hit, want, _ = scene_setup(*wl)
-    saved = tracer.config()
-    try:
-        for extra in ({"waves_per_cu": 4}, {"waves_per_cu": 20}, {"num_queues": 1, "fetch_threshold": 48, "waves_per_cu": 8}):
-            tracer.set_config(**{**saved, "tail_lanes": 16, "handoff": handoff, "autotune": 0, **extra})
-            for _ in range(2):
-                res, _ = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=True)
-                info = tracer.last_info
-                assert info["handoff"] == handoff and info["stack_overflows"] == 0
-                if any_hit:
-                    assert_valid_hits(rays, res, want, bufs)
-                else:
-                    assert np.array_equal(res[:, :2], want[:, :2]), f"{extra}: closest hits differ"
-    finally:
-        tracer.set_config(**saved)
-
-
-def test_workgroup_handoff_streams_and_comb(tracer):
-    """Hand-off launches back to back on two streams, and the comb scene whose deep rays keep
-    their stacks in the spill slab (those stay with their wave) next to shallow ones."""
-    from mrt.tracer import GpuBvh, RayBuffer
-    bufs, rays, _, want, _ = scene_setup("hairball:800", 256, 192, "diffuse")
-    saved = tracer.config()
-    try:
-        tracer.set_config(tail_lanes=16, handoff=4, autotune=0, waves_per_cu=8)
-        tracer.set_bvh(GpuBvh(bufs))
-        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
-        rbs = [RayBuffer(rays, need_closest_hit=True) for _ in range(6)]
-        torch.cuda.synchronize()
-        for k, rb in enumerate(rbs):
-            s = s1 if k % 2 == 0 else s2
-            with torch.cuda.stream(s):
-                tracer.trace_async(rb, exact_rcp=True, stream=s)
-        s1.synchronize()
-        s2.synchronize()
-        for rb in rbs:
-            assert np.array_equal(rb.results_numpy()[:, :2], want[:, :2])
-        cb, ray, expect = kat.scene_comb(40)
-        tracer.set_bvh(GpuBvh(cb))
-        rb = RayBuffer(np.stack([ray] * 3000), need_closest_hit=True)
-        tracer.trace_batch(rb, exact_rcp=True)
-        res = rb.results_numpy()
-        assert tracer.last_info["stack_overflows"] == 0
-        assert (res[:, 0] == expect[0]).all() and (res[:, 1] == kat.f2i(expect[1])).all()
-    finally:
-        tracer.set_config(**saved)
-
-
 def fuzz_rays(scene, n, seed, w=96, h=72):
     """Incoherent rays inside a scene (test_random_rays_fuzz's recipe)."""
     bufs, base, _, _, _ = scene_setup(scene, w, h, "primary")
