@@ -480,6 +480,8 @@ int refresh_wide(mrt_tracer* t) {
 // reproducible run pins the schedule: autotune 0, or the schedules saved per BVH
 // (mrt_tracer_tune_export / _import, mrt/tuned_schedules.json for the bench).
 constexpr int kMaxTuned = 64;   // batch sizes tuned per handle; others use the rule
+constexpr int kXcdQueueBlock = 4096;   // candidate 2's per-XCD queue blocks (rays) and shared tail (%)
+constexpr int kXcdQueueShared = 5;
 
 mrt_launch_cfg tune_candidate(const mrt_launch_cfg& base, int c, int stage1) {
     if (c >= TuneState::kSchedules) {
@@ -500,10 +502,22 @@ mrt_launch_cfg tune_candidate(const mrt_launch_cfg& base, int c, int stage1) {
     x.fetch_threshold = 0;
     x.waves_per_cu = 0;
     x.num_queues = -1;
+    x.queue_block = 0;
+    x.queue_shared = 0;
     switch (c) {
         case 0: break;                                                      // static rounds, 20 waves/CU
         case 1: x.waves_per_cu = 8; break;                                  // static rounds, fewer waves
-        case 2: x.num_queues = 8; break;                                    // per-XCD queues
+        case 2:   // per-XCD queues of 4096-ray blocks dealt cyclically (every XCD samples the whole frame,
+                  // its L2 holds its own blocks' nodes and triangles), the last 5 % in one shared queue,
+                  // refills at 48 live lanes, 20 waves/CU: a multi-million-ray launch over a BVH above the
+                  // Infinity Cache (hairball 2 M rays: 0.630 -> 0.547 ms, fabric bytes 1.07 -> 0.74 GB;
+                  // profiles/round4_queue_ab.txt)
+            x.num_queues = 8;
+            x.queue_block = kXcdQueueBlock;
+            x.queue_shared = kXcdQueueShared;
+            x.fetch_threshold = kBigQueueThreshold;
+            x.waves_per_cu = kStridedWaves;
+            break;
         case 3: x.num_queues = 1; x.fetch_threshold = kBigQueueThreshold; x.waves_per_cu = kBigQueueWaves; break;   // global queue
         case 4: x.num_queues = 1; x.fetch_threshold = 48; x.waves_per_cu = 12; break;
         case 5: x.waves_per_cu = 16; break;

@@ -96,7 +96,7 @@ typedef struct mrt_launch_cfg {
     int32_t autotune;          /* 1 = with the distribution knobs above at their defaults, the first launches
                                   of each batch size (per kernel variant, up to 64 sizes) time eight ray-
                                   distribution schedules (static rounds at 20, 16, 12 or 8 waves/CU, per-XCD
-                                  queues, the global queue at 20, 16 or 12 waves/CU), then
+                                  block-cyclic queues, the global queue at 20, 16 or 12 waves/CU), then
                                   the winner with spec_slack 4 and 6, without the frontier tail and with 16
                                   lane groups (each
                                   knob only when left at its default), eight times each without blocking,
@@ -161,7 +161,7 @@ typedef struct mrt_tuned_schedule {
     int32_t candidate;
     int32_t version;           /* MRT_TUNE_VERSION when exported; others are refused on import */
 } mrt_tuned_schedule;
-enum { MRT_TUNE_VERSION = 6 };
+enum { MRT_TUNE_VERSION = 7 };
 
 /* ---- handle API -------------------------------------------------------- */
 int  mrt_tracer_create(int device, mrt_tracer** out);

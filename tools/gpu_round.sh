@@ -39,10 +39,10 @@ for step in "$@"; do
     tune)
       rm -f $O/tuned_schedules.json
       W=""; for w in $BENCH_WL; do [ $w = hairball-diffuse-1920x1080 ] || W="$W --workload $w"; done
-      timeout -k 10 900 python -u tools/tune_db.py $W --out $O/tuned_schedules.json > $O/tune_db.txt 2> $O/tune_db.err || fail tune_db $O/tune_db.err
-      timeout -k 10 300 python -u tools/tune_db.py --workload hairball-diffuse-1920x1080 --margin 0.015 --out $O/tuned_schedules.json \
+      timeout -k 10 720 python -u tools/tune_db.py $W ${TUNE_ARGS} --out $O/tuned_schedules.json > $O/tune_db.txt 2> $O/tune_db.err || fail tune_db $O/tune_db.err
+      timeout -k 10 240 python -u tools/tune_db.py --workload hairball-diffuse-1920x1080 --margin 0.015 ${TUNE_ARGS} --out $O/tuned_schedules.json \
         >> $O/tune_db.txt 2>> $O/tune_db.err || fail "tune hairball" $O/tune_db.err
-      timeout -k 10 300 python -u tools/tune_db.py --workload bunny-primary-1024x768 --fast-rcp --out $O/tuned_schedules.json \
+      timeout -k 10 180 python -u tools/tune_db.py --workload bunny-primary-1024x768 --fast-rcp ${TUNE_ARGS} --out $O/tuned_schedules.json \
         >> $O/tune_db.txt 2>> $O/tune_db.err || fail "tune fast" $O/tune_db.err
       cut -c1-300 $O/tune_db.txt ;;
     profile)
