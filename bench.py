@@ -55,7 +55,7 @@ L2_PEAK_GBS = 34500.0    # the eight XCD L2s together (§L2)
 LINE_BYTES = 128         # gfx950 L1 and L2 line: one TCP_TCC_READ_REQ / TCC_EA0_RDREQ per line
                          # (tools/ubench_levels.hip, profiles/round3_counter_calibration.md)
 MALL_BYTES = 256 << 20   # Infinity Cache: a BVH above this streams from HBM
-PROFILE_TAGS = ("round4", "round3")   # committed rocprofv3 summaries the line may cite, newest first
+PROFILE_TAGS = ("round4",)   # committed rocprofv3 summaries the line may cite, newest first
                                       # (profiles/<tag>_<workload>_*): only one of the timed schedule is cited
 LINE_MAX_BYTES = 10_000  # the driver parses one stdout line; round 3's 21.7 kB line was not parsed
 STORE = None             # mrt.schedules.ScheduleStore the tracer's schedules are locked from (main())
