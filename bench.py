@@ -697,7 +697,7 @@ def run_workload(name, tracer, scenes, world, rank, steps, warmup, exact, want_c
     return out
 
 
-def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact):
+def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofline=False):
     """one fixed RayBuffer (the hairball diffuse frame at 8 spp,
     generated by the Renderer's <= 2^21-ray batches with their glibc seeds), cut
     into shards — block-cyclic (STRONG["block"]-ray blocks dealt round-robin to
@@ -741,6 +741,14 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact):
 
     launches = shard_steps(local)
     wall, launch_ms, _ = time_steps(launches, steps, warmup, world)
+    shard_roofline = None
+    if with_roofline:   # the line's roofline at N > 1: this rank's launches (SURVEY §8(d) bytes, per launch)
+        views = [(local.view(a, b), 0) for a, b in shard_launches(0, local.size, cfg["max_batch"], cfg["min_launches"])]
+        alg, _, _, _ = algorithmic_bytes(tracer, views)
+        sched = schedule_of(tracer, views[0][0], exact)
+        shard_roofline = roofline("hairball-diffuse-1920x1080", alg / len(views), launch_ms, e["gbvh"].total_bytes, sched)
+        shard_roofline["note"] = (f"rank {rank}'s {len(views)} launches of <= {cfg['max_batch']} rays on "
+                                  f"{len(streams)} streams; kernel_ms = one launch alone")
     per_rank = gather_floats(wall / steps * 1e3, world)
     tn = max(per_rank)
     # gather of this shard's {id, t} to rank 0 (RCCL point-to-point; gloo: via host),
@@ -791,6 +799,7 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact):
         "gathered_equals_single_gpu": equal, "streams": len(streams), "min_launches": cfg["min_launches"],
         "shards": f"block-cyclic, {cfg['block']}-ray blocks" if cfg["block"] > 0 else "contiguous",
         "projected_from_one_gpu": projected,
+        "roofline": shard_roofline,
         "collective": f"{DIST_BACKEND} point-to-point gather of {n * 8} B to rank 0" if world > 1 else None,
     }
 
@@ -882,7 +891,7 @@ def make_line(args, world, head, extras, strong, tracer_cfg):
         "dtype": "f32",
         "data": "synthetic (deterministic stand-in scene with the README triangle count; rays generated on the device)",
         "config": config,
-        "roofline": compact_roofline(head["roofline"]) if args.scaling == "weak" else None,
+        "roofline": compact_roofline(head["roofline"] if args.scaling == "weak" else strong.get("roofline")),
         "cpu_baseline": ({k: head["cpu_baseline"][k] for k in ("value", "unit", "cores", "kind", "sample", "cpu_model")}
                          if head.get("cpu_baseline") else None),
         "parity": compact_parity(head.get("cpu_baseline"), head.get("rcp_fast")),
@@ -995,7 +1004,8 @@ def main():
         STRONG["min_launches"] = max(1, args.strong_min_launches)
         STRONG["block"] = max(0, args.strong_block)
         STRONG["streams"] = args.strong_streams
-        strong = strong_scaling(tracer, scenes, world, rank, args.strong_steps, 3, exact)
+        strong = strong_scaling(tracer, scenes, world, rank, args.strong_steps, 3, exact,
+                                with_roofline=args.scaling == "strong")
         log(f"[strong] {strong['workload']} n={world}: T1 {strong['t1_ms']} ms, Tn {strong['tn_ms']} ms, "
             f"eta {strong['eta']} (with gather {strong['eta_with_gather']}); projected from one GPU: "
             f"{ {k: v['eta'] for k, v in (strong['projected_from_one_gpu'] or {}).items()} }")
