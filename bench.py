@@ -105,7 +105,7 @@ EXTRA_N1 = ["bunny-primary-640x480", "conference-ao-640x480", "sponza-diffuse-64
 # Strong-scaling config: scene, frame, samples per pixel, rays per launch.
 # min_launches: a shard is cut into at least this many launches (alternating over two streams).
 STRONG = {"name": "hairball-diffuse-1920x1080x8spp", "scene": "hairball", "w": 1920, "h": 1080, "spp": 8,
-          "max_batch": 1 << 21, "min_launches": 1, "block": 1 << 14, "streams": 2}
+          "max_batch": 1 << 21, "min_launches": 1, "block": 1 << 14, "streams": 2, "balance": True}
 STRONG_PROJECT = (2, 4, 8)   # N=1 only: rank counts whose per-rank shards are timed on the one GPU
 
 
@@ -706,7 +706,7 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
     whole buffer alone, same run; then the {id, t} gather to rank 0, checked
     against the single-GPU results."""
     import torch
-    from mrt.dist import gather_results, local_rays, shard_launches, shard_spans
+    from mrt.dist import balance_blocks, block_weights, gather_results, local_rays, shard_launches, shard_spans
     from mrt.raygen import RAY_DIFFUSE
     from mrt.renderer import Renderer
     from mrt.tracer import RayBuffer
@@ -723,10 +723,23 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
     big = RayBuffer(torch.cat([b.rays for b in parts]), need_closest_hit=True)
     del parts, r
 
+    # Blocks dealt by live-ray count (balance_blocks) or cyclically: every rank
+    # computes the same deal from the buffer's tmax column (one reduction).
+    weights = block_weights(big.rays, cfg["block"]) if cfg["balance"] and cfg["block"] > 0 else None
+    deals = {}
+
+    def owners_for(k):
+        if weights is None or k == 1:
+            return None
+        if k not in deals:
+            deals[k] = balance_blocks(weights, k)
+        return deals[k]
+
     def shard_buffer(k, rk):
         # the shard as one contiguous RayBuffer (built before the timed region: a
         # rank generating its own rays would produce it in this order directly)
-        return RayBuffer(local_rays(big.rays, shard_spans(n, k, rk, cfg["block"])), need_closest_hit=True)
+        return RayBuffer(local_rays(big.rays, shard_spans(n, k, rk, cfg["block"], owners_for(k))),
+                         need_closest_hit=True)
 
     local = big if world == 1 else shard_buffer(world, rank)
     torch.cuda.synchronize()
@@ -735,12 +748,17 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
     # launch's tail overlaps the next one's start.
     streams = [torch.cuda.current_stream(), torch.cuda.Stream()][:cfg["streams"]]
 
-    def shard_steps(buf):
-        return [tracer.launcher(buf.view(a, b), exact_rcp=exact, stream=streams[i % len(streams)])
+    def shard_steps(buf, nstreams=len(streams)):
+        return [tracer.launcher(buf.view(a, b), exact_rcp=exact, stream=streams[i % nstreams])
                 for i, (a, b) in enumerate(shard_launches(0, buf.size, cfg["max_batch"], cfg["min_launches"]))]
 
     launches = shard_steps(local)
     wall, launch_ms, _ = time_steps(launches, steps, warmup, world)
+    one_stream_ms = None
+    if world == 1 and len(streams) > 1:
+        # the same launches on one stream: the autotuner's (or saved) schedule applies
+        w1s, _, _ = time_steps(shard_steps(local, 1), steps, warmup, 1)
+        one_stream_ms = w1s / steps * 1e3
     shard_roofline = None
     if with_roofline:   # the line's roofline at N > 1: this rank's launches (SURVEY §8(d) bytes, per launch)
         views = [(local.view(a, b), 0) for a, b in shard_launches(0, local.size, cfg["max_batch"], cfg["min_launches"])]
@@ -754,12 +772,12 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
     # gather of this shard's {id, t} to rank 0 (RCCL point-to-point; gloo: via host),
     # after one untimed gather (RCCL creates its point-to-point communicators on first use)
     if world > 1:
-        gather_results(local.results if DIST_BACKEND == "nccl" else local.results.cpu(), n, block=cfg["block"])
+        gather_results(local.results if DIST_BACKEND == "nccl" else local.results.cpu(), n, block=cfg["block"], owners=owners_for(world))
     torch.cuda.synchronize()
     barrier(world)
     t0 = time.perf_counter()
     res = local.results if DIST_BACKEND == "nccl" else local.results.cpu()
-    full = gather_results(res, n, block=cfg["block"]) if world > 1 else big.results[:, :2]
+    full = gather_results(res, n, block=cfg["block"], owners=owners_for(world)) if world > 1 else big.results[:, :2]
     torch.cuda.synchronize()
     gather_ms = reduce_over_ranks(1e3 * (time.perf_counter() - t0), world) if world > 1 else 0.0
     # T_1 in the same run: rank 0 alone over the whole buffer (the others wait)
@@ -793,11 +811,13 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
         "workload": cfg["name"], "rays_traced": n, "rays_counted": counted, "launch_rays_max": cfg["max_batch"],
         "shard_rays": local.size, "n_gpus": world, "t1_ms": round(t1, 4), "tn_ms": round(tn, 4),
         "per_rank_ms": [round(x, 4) for x in per_rank], "kernel_ms_per_launch": round(launch_ms, 4),
+        "one_stream_ms": None if one_stream_ms is None else round(one_stream_ms, 4),
         "eta": round(t1 / (world * tn), 4), "gather_ms": round(gather_ms, 3),
         "eta_with_gather": round(t1 / (world * (tn + gather_ms)), 4),
         "value": round(counted / (tn * 1e-3) / 1e6, 2), "value_with_gather": round(counted / ((tn + gather_ms) * 1e-3) / 1e6, 2),
         "gathered_equals_single_gpu": equal, "streams": len(streams), "min_launches": cfg["min_launches"],
-        "shards": f"block-cyclic, {cfg['block']}-ray blocks" if cfg["block"] > 0 else "contiguous",
+        "shards": ((f"{cfg['block']}-ray blocks dealt by live-ray count" if weights is not None
+                    else f"block-cyclic, {cfg['block']}-ray blocks") if cfg["block"] > 0 else "contiguous"),
         "projected_from_one_gpu": projected,
         "roofline": shard_roofline,
         "collective": f"{DIST_BACKEND} point-to-point gather of {n * 8} B to rank 0" if world > 1 else None,
@@ -928,6 +948,8 @@ def main():
     ap.add_argument("--strong-steps", type=int, default=10)
     ap.add_argument("--strong-block", type=int, default=STRONG["block"],
                     help="block-cyclic shard block (rays); 0 = contiguous shards")
+    ap.add_argument("--strong-balance", type=int, default=int(STRONG["balance"]), choices=[0, 1],
+                    help="1: deal the shard blocks by live-ray count (mrt.dist.balance_blocks); 0: cyclically")
     ap.add_argument("--strong-streams", type=int, default=STRONG["streams"], choices=[1, 2],
                     help="caller streams the strong-scaling launches alternate over")
     ap.add_argument("--strong-min-launches", type=int, default=STRONG["min_launches"],
@@ -1004,6 +1026,7 @@ def main():
         STRONG["min_launches"] = max(1, args.strong_min_launches)
         STRONG["block"] = max(0, args.strong_block)
         STRONG["streams"] = args.strong_streams
+        STRONG["balance"] = bool(args.strong_balance)
         strong = strong_scaling(tracer, scenes, world, rank, args.strong_steps, 3, exact,
                                 with_roofline=args.scaling == "strong")
         log(f"[strong] {strong['workload']} n={world}: T1 {strong['t1_ms']} ms, Tn {strong['tn_ms']} ms, "

@@ -480,6 +480,7 @@ int refresh_wide(mrt_tracer* t) {
 // reproducible run pins the schedule: autotune 0, or the schedules saved per BVH
 // (mrt_tracer_tune_export / _import, mrt/tuned_schedules.json for the bench).
 constexpr int kMaxTuned = 64;   // batch sizes tuned per handle; others use the rule
+constexpr int64_t kTuneInherit = 32;   // a new batch size within 1/32 of a settled one takes its schedule
 constexpr int kXcdQueueBlock = 4096;   // candidate 2's per-XCD queue blocks (rays) and shared tail (%)
 constexpr int kXcdQueueShared = 5;
 
@@ -618,14 +619,29 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
             tune->stream = stream;
             // the candidate that equals the fixed rule for this batch (effective_cfg)
             tune->rule = cfg.num_queues == 1 ? (cfg.waves_per_cu == kBigQueueWaves ? 3 : 4) : 0;
+            // A batch within 1/kTuneInherit of a settled batch size of the same variant takes
+            // that schedule instead of exploring (the nearest one): the strong-scaling shards of
+            // one frame differ by a block or two (2,064,384 .. 2,080,768 rays against the saved
+            // 2,073,600), and ~100 exploring launches per shard size would fall in the timed steps.
+            int64_t bestGap = -1;
+            for (const auto& kv : t->tunes) {
+                if (kv.first.second != key.second || kv.second->locked < 0) continue;
+                const int64_t gap = std::llabs((int64_t)kv.first.first - numRays);
+                if (gap * kTuneInherit > (int64_t)kv.first.first || (bestGap >= 0 && gap >= bestGap)) continue;
+                bestGap = gap;
+                tune->stage1 = kv.second->stage1;
+                tune->locked = kv.second->locked;
+            }
             t->tunes[key] = tune;
         }
-        // A batch size launched on several streams keeps the fixed rule: its launches
-        // overlap, and a schedule's time alone no longer ranks the pipeline (the
-        // bench's two-stream hairball buffer: 5.2 ms on the rule, 6.2 tuned alone).
+        // A batch size launched on several streams is not explored there: its launches
+        // overlap, and a candidate's time alone no longer ranks the pipeline. It runs its
+        // settled schedule (saved, inherited, or settled on one stream) if it has one, else
+        // the fixed rule (the bench's two-stream hairball 8 spp buffer: 4.23 ms on the rule,
+        // 3.48 on the per-XCD block-cyclic schedule).
         if (tune && !tune->stream) tune->stream = stream;   // an imported schedule: first used here
         if (tune && tune->stream != stream) tune->multiStream = true;
-        if (tune && tune->multiStream) tune = nullptr;
+        if (tune && tune->multiStream && tune->locked < 0) tune = nullptr;
     }
     if (tune) {
         tune_collect(tune);

@@ -2,7 +2,8 @@
 every rank, the RayBuffer is split into shards (contiguous ranges, or
 block-cyclic blocks so that every shard samples the whole frame), every rank
 traces its shard with its own persistent grid, and hit results are gathered to
-the root only when the caller needs them in one place.
+the root only when the caller needs them in one place. Blocks can be dealt by
+live-ray weight (balance_blocks) instead of cyclically.
 
 One process per GPU over torch.distributed ("nccl" = RCCL on ROCm; "gloo"
 for the CPU tests). The trace itself needs no collective.
@@ -27,18 +28,67 @@ def shard_range(n: int, world: int, rank: int) -> tuple[int, int]:
     return lo, lo + base + (1 if rank < extra else 0)
 
 
-def shard_spans(n: int, world: int, rank: int, block: int = 0) -> list[tuple[int, int]]:
+def block_weights(rays: torch.Tensor, block: int) -> torch.Tensor:
+    """Live rays per block-ray block of a RayBuffer (float32 [n, 8]): rays whose
+    tmax is not negative. The AO/diffuse generators give the samples of a pixel
+    whose primary ray missed tmax = -1 (RayGenKernels.cu:117-227); the trace
+    retires such a ray at once, so a block's cost follows its live rays. One
+    reduction over the tmax column, on the buffer's device."""
+    if block <= 0:
+        raise ValueError("block_weights: block must be positive")
+    n = rays.shape[0]
+    live = (rays[:, 7] >= 0).to(torch.int64)
+    pad = (-n) % block
+    if pad:
+        live = torch.cat([live, live.new_zeros(pad)])
+    return live.view(-1, block).sum(1)
+
+
+def balance_blocks(weights, world: int) -> np.ndarray:
+    """Owner rank of every block (int32 [nblocks]): the blocks in decreasing weight
+    (ties: lower index first) dealt in serpentine order — ranks 0..world-1, then
+    world-1..0, and so on. Every rank gets the same number of blocks (±1), so the
+    shards hold the same number of rays, and the live rays balance to within one
+    block's weight (a pure weight-greedy deal hands all the dead blocks to one
+    rank: retiring 10 M dead rays took 1.9 ms on one MI355X). Deterministic, so
+    every rank computes the same owners from the same weights. Used with
+    shard_spans(..., owners=...): each rank keeps its blocks in frame order."""
+    w = np.asarray(weights.cpu() if isinstance(weights, torch.Tensor) else weights, dtype=np.int64)
+    if w.ndim != 1 or world < 1:
+        raise ValueError("balance_blocks: 1-D weights and world >= 1 expected")
+    order = np.argsort(-w, kind="stable")
+    j = np.arange(len(w))
+    pos, rnd = j % world, j // world
+    owners = np.empty(len(w), dtype=np.int32)
+    owners[order] = np.where(rnd % 2 == 0, pos, world - 1 - pos)
+    return owners
+
+
+def shard_spans(n: int, world: int, rank: int, block: int = 0, owners=None) -> list[tuple[int, int]]:
     """The ray ranges of `rank`'s shard of n rays. block = 0: one contiguous range
     (shard_range). block > 0: block-cyclic — the buffer cut into block-ray blocks,
     block i to rank i % world — so every shard draws from the whole frame. A
     frame's RayBuffer is in pixel order (AO/diffuse samples of a pixel adjacent,
     RayGenKernels.cu:117-227), so contiguous shards are image regions of unequal
     cost: on the hairball 1920x1080x8spp buffer the 8 contiguous shards took
-    0.59-1.12 ms on one MI355X, which caps eta(8) at 0.54."""
+    0.59-1.12 ms on one MI355X, which caps eta(8) at 0.54. owners (block > 0):
+    block i to rank owners[i] instead (balance_blocks), adjacent blocks merged."""
     if block <= 0 or world == 1:
         lo, hi = shard_range(n, world, rank)
         return [(lo, hi)] if hi > lo else []
-    return [(a, min(n, a + block)) for a in range(rank * block, n, world * block)]
+    if owners is None:
+        return [(a, min(n, a + block)) for a in range(rank * block, n, world * block)]
+    owners = np.asarray(owners)
+    if len(owners) != -(-n // block):
+        raise ValueError(f"shard_spans: {len(owners)} block owners for {-(-n // block)} blocks of {block} rays")
+    spans: list[tuple[int, int]] = []
+    for i in np.flatnonzero(owners == rank):
+        a, b = int(i) * block, min(n, (int(i) + 1) * block)
+        if spans and spans[-1][1] == a:
+            spans[-1] = (spans[-1][0], b)
+        else:
+            spans.append((a, b))
+    return spans
 
 
 def spans_index(spans, device=None) -> torch.Tensor:
@@ -118,20 +168,22 @@ def shard_launches(lo: int, hi: int, max_rays: int, min_launches: int = 1):
 
 
 def trace_shard(tracer, rays, world: int, rank: int, max_rays: int = 1 << 21, exact_rcp: bool = True,
-                stream=None, block: int = 0):
+                stream=None, block: int = 0, owners=None):
     """Strong-scaling step of one rank: trace its shard of the RayBuffer `rays`
     (every rank holds the same buffer) in launches of at most max_rays rays,
     stream-ordered. block = 0: the contiguous shard, results written in place;
     returns (lo, hi). block > 0: the block-cyclic shard, gathered into a local
     RayBuffer first; returns that buffer (its results are the shard's, in
-    shard_spans order — what gather_results(..., block=block) expects)."""
+    shard_spans order — what gather_results(..., block=block, owners=owners)
+    expects). owners: balance_blocks' deal of the blocks, or None (cyclic)."""
     if block <= 0:
         lo, hi = shard_range(rays.size, world, rank)
         for a, b in shard_launches(lo, hi, max_rays):
             tracer.trace_async(rays.view(a, b), exact_rcp=exact_rcp, stream=stream)
         return lo, hi
     from .tracer import RayBuffer
-    local = RayBuffer(local_rays(rays.rays, shard_spans(rays.size, world, rank, block)), rays.need_closest_hit)
+    local = RayBuffer(local_rays(rays.rays, shard_spans(rays.size, world, rank, block, owners)),
+                      rays.need_closest_hit)
     if stream is not None:
         # the local buffer was built on the current stream: the launches on `stream` wait for it
         stream.wait_stream(torch.cuda.current_stream())
@@ -140,7 +192,7 @@ def trace_shard(tracer, rays, world: int, rank: int, max_rays: int = 1 << 21, ex
     return local
 
 
-def gather_results(local: torch.Tensor, n_total: int, dst: int = 0, block: int = 0):
+def gather_results(local: torch.Tensor, n_total: int, dst: int = 0, block: int = 0, owners=None):
     """Gather every rank's RayResult shard (int32 [k, 4], the shard's rays in
     shard_spans order) to rank `dst` in ray order with point-to-point send/recv
     (RCCL has no gather primitive; the root receives from all peers at once over
@@ -153,7 +205,7 @@ def gather_results(local: torch.Tensor, n_total: int, dst: int = 0, block: int =
                         f"{tuple(local.shape)}")
     if dist.get_backend() == "nccl" and not _on_device(local):
         raise ValueError("gather_results: RCCL (nccl) moves device tensors; got a " + local.device.type + " tensor")
-    mine = sum(b - a for a, b in shard_spans(n_total, world, rank, block))
+    mine = sum(b - a for a, b in shard_spans(n_total, world, rank, block, owners))
     if local.shape[0] != mine:
         raise ValueError(f"gather_results: rank {rank} holds {local.shape[0]} results, its shard of {n_total} "
                          f"rays has {mine}")
@@ -165,7 +217,7 @@ def gather_results(local: torch.Tensor, n_total: int, dst: int = 0, block: int =
     full = torch.empty((n_total, 2), dtype=torch.int32, device=local.device)
     reqs, scatter = [], []
     for r in range(world):
-        spans = shard_spans(n_total, world, r, block)
+        spans = shard_spans(n_total, world, r, block, owners)
         count = sum(b - a for a, b in spans)
         if count == 0:
             continue

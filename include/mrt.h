@@ -102,8 +102,10 @@ typedef struct mrt_launch_cfg {
                                   knob only when left at its default), eight times each without blocking,
                                   after one untimed round of them; the median ranks them and a candidate
                                   replaces the fixed rule (stage 1) or the stage-1 winner (stage 2) only
-                                  when 3 % faster. A batch size launched on more than one stream keeps the
-                                  fixed rule; reset by bind and set_config (default 1; mrt_tracer_tune_export /
+                                  when 3 % faster. A new batch size within 1/32 of a settled one (same
+                                  variant) takes the nearest settled schedule without exploring. A batch
+                                  size launched on more than one stream is not explored: it runs its settled
+                                  schedule if it has one, else the fixed rule; reset by bind and set_config (default 1; mrt_tracer_tune_export /
                                   _import save and restore the choices). 0 = the fixed rule only; -1 = default */
     int32_t tail_lanes;        /* exact 4-wide speculative traversal: a wave that cannot refill (its strided
                                   round, or its queue drained) and is down to at most this many tracing

@@ -183,3 +183,49 @@ def test_shard_layout_covers_every_ray_once(world, block):
         assert all(b - a <= 1 << 16 for a, b in launches)
         assert all(launches[i][1] == launches[i + 1][0] for i in range(len(launches) - 1))
     assert bool((seen == 1).all())
+
+
+def test_balance_blocks_deals_equal_counts_and_live_rays():
+    """balance_blocks: every block owned once; the ranks get the same number of blocks
+    (±1) and live rays within one block's weight; the same weights give the same deal."""
+    rng = np.random.default_rng(3)
+    for nblocks, world in ((1013, 8), (1013, 3), (7, 8), (64, 1), (0, 4)):
+        w = rng.integers(0, 16385, size=nblocks)
+        w[: nblocks // 4] = 0                       # dead blocks (sky) in one region
+        owners = D.balance_blocks(torch.from_numpy(w), world)
+        assert owners.shape == (nblocks,) and np.array_equal(owners, D.balance_blocks(w, world))
+        counts = np.bincount(owners, minlength=world)
+        loads = np.bincount(owners, weights=w, minlength=world)
+        if nblocks:
+            assert counts.max() - counts.min() <= 1
+            assert loads.max() - loads.min() <= w.max()
+
+
+def test_block_weights_count_live_rays():
+    rays = torch.zeros((10, 8))
+    rays[:, 7] = torch.tensor([1.0, -1.0, 0.0, 5.0, -1.0, -1.0, 2.0, 3.0, -1.0, 1.0])
+    assert D.block_weights(rays, 4).tolist() == [3, 2, 1]
+    with pytest.raises(ValueError):
+        D.block_weights(rays, 0)
+
+
+@pytest.mark.parametrize("world,block", [(2, 1000), (8, 4096), (3, 777)])
+def test_gather_results_with_a_weighted_deal(fake, world, block):
+    """Shards dealt by balance_blocks gather back into ray order (nccl branch)."""
+    n = 100_003
+    full_ref = results_for(n)
+    nblocks = -(-n // block)
+    owners = D.balance_blocks(np.random.default_rng(world).integers(0, block, nblocks), world)
+    seen = torch.zeros(n, dtype=torch.int32)
+    for r in range(world):
+        seen[D.spans_index(D.shard_spans(n, world, r, block, owners))] += 1
+    assert bool((seen == 1).all())
+    f = fake(world)
+
+    def rank_fn(r):
+        idx = D.spans_index(D.shard_spans(n, world, r, block, owners))
+        return D.gather_results(full_ref[idx].contiguous(), n, dst=0, block=block, owners=owners)
+    out = f.run(rank_fn)
+    assert torch.equal(out[0], full_ref[:, :2])
+    with pytest.raises(ValueError, match="block owners"):
+        D.shard_spans(n, world, 0, block, owners[:-1])

@@ -175,6 +175,45 @@ def test_autotuned_schedule_settles_and_keeps_results(env):
     assert np.array_equal(rb.results_numpy()[:, :2], want[:, :2])
 
 
+def test_nearby_batch_sizes_and_other_streams_take_the_settled_schedule(env):
+    """A batch size within 1/32 of a settled one takes its schedule at once (the
+    strong-scaling shards of one frame differ by a block or two); a settled batch
+    size launched on a second stream keeps its schedule instead of falling back to
+    the fixed rule; one beyond 1/32 explores. Results equal the oracle throughout."""
+    bench, scenes, tracer, threads = env
+    name = "bunny-primary-1024x768"
+    e = scenes.get(bench.workload_spec(name)[0])
+    bufs = scenes.host_buffers(bench.workload_spec(name)[0])
+    rb = bench.Batches(name, e["scene"], e["gbvh"], tracer).batches[0][0]
+    tracer.set_config(autotune=1)   # a fresh tuning state
+    n = rb.size
+    ref = rb.view(0, n)
+    for _ in range(200):            # settle size n
+        tracer.trace_batch(ref, exact_rcp=True)
+        if tracer.last_info["autotune_locked"]:
+            break
+    assert tracer.last_info["autotune_locked"] == 1
+    chosen = tracer.last_info["autotune_candidate"]
+    want, _, _ = O.trace(rb.rays.cpu().numpy(), *bufs, threads=threads)
+    # a batch 1/64 smaller: inherits the lock on its first launch
+    near = rb.view(0, n - n // 64)
+    tracer.trace_batch(near, exact_rcp=True)
+    assert tracer.last_info["autotune_locked"] == 1 and tracer.last_info["autotune_candidate"] == chosen
+    assert np.array_equal(near.results_numpy()[:, :2], want[: near.size, :2])
+    # the settled size on a second stream: still its schedule
+    s2 = torch.cuda.Stream()
+    tracer.trace_batch(ref, exact_rcp=True, stream=s2)
+    torch.cuda.synchronize()
+    assert tracer.last_info["autotune_locked"] == 1 and tracer.last_info["autotune_candidate"] == chosen
+    assert np.array_equal(ref.results_numpy()[:, :2], want[:, :2])
+    # a batch 1/8 smaller: too far, it explores
+    far = rb.view(0, n - n // 8)
+    tracer.trace_batch(far, exact_rcp=True)
+    assert tracer.last_info["autotune_locked"] == 0
+    assert np.array_equal(far.results_numpy()[:, :2], want[: far.size, :2])
+    tracer.set_bvh(e["gbvh"])
+
+
 # SURVEY §8(a) Note 3 bounds: the "edge" class (an accept/reject flip of one triangle under
 # +-1 ulp of 1/Dz) at most 1e-6 of a workload's rays, and never more than one ray below 1e6 rays
 EDGE_FRACTION = 1e-6

@@ -39,6 +39,19 @@ def main():
             runs.append(rb.stats.cpu().numpy().astype(np.int64))
         # the run with the median last end
         ends = [r[:, 1].max() - r[:, 0].min() for r in runs]
+        if os.environ.get("TL2"):
+            # MRT_TAIL_TIMELINE=2 build: field 0 holds the ticks spent popping the home stack
+            st = runs[0]
+            tail = st[:, 2] != 0
+            iters = np.maximum(1, st[:, 3] & 0xFFFF)
+            per_it = (st[:, 1] - st[:, 2]) * 0.01 / iters
+            pop = st[:, 0] * 0.01 / iters
+            mem = ((st[:, 3] >> 16) & 0xFFFF) * 0.01 / iters
+            print(f"{wl} {cfg}: kernel {plain:.4f} ms; {tail.sum()} tail rays; us per tail iteration median "
+                  f"{np.median(per_it[tail]):.3f} (node/leaf loads {np.median(mem[tail]):.3f}, pop "
+                  f"{np.median(pop[tail]):.3f}); p90 {np.percentile(per_it[tail], 90):.3f} (loads "
+                  f"{np.percentile(mem[tail], 90):.3f}, pop {np.percentile(pop[tail], 90):.3f})", flush=True)
+            continue
         st = runs[int(np.argsort(ends)[len(ends) // 2])]
         t0 = st[:, 0].min()
         start, end = (st[:, 0] - t0) * 0.01, (st[:, 1] - t0) * 0.01
