@@ -79,10 +79,17 @@ def run(args, workload):
                                    g.tri_index.data_ptr(), g.tri_index_bytes) == 0
         c = _lib.LaunchCfg()
         assert lib.mrt_tracer_get_config(h, C.byref(c)) == 0
-        for k, v in json.loads(cfg or "{}").items():
+        knobs = json.loads(cfg or "{}")
+        saved = knobs.pop("saved", 0)   # "saved": 1 = lock the BVH's saved schedules (mrt/tuned_schedules.json)
+        for k, v in knobs.items():
             setattr(c, k, v)
         rc = lib.mrt_tracer_set_config(h, C.byref(c))
         assert rc == 0, f"config {cfg} rejected"
+        if saved:
+            from mrt.schedules import ScheduleStore
+            ent = ScheduleStore().entries(g.fingerprint)
+            arr = (_lib.TunedSchedule * max(1, len(ent)))(*[_lib.TunedSchedule(*x) for x in ent])
+            assert lib.mrt_tracer_tune_import(h, arr, len(ent)) == 0, "saved schedules rejected"
         variants.append((spec, lib, h))
     ref = None
     times = {spec: [] for spec, _, _ in variants}
