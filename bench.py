@@ -19,9 +19,9 @@ replicated). Two scalings are measured in every run:
   * strong (BASELINE configs[4]; the line's value at N > 1): ONE
     fixed RayBuffer — hairball diffuse 1920x1080 x 8 spp = 16.6 M rays, generated
     as the reference's Renderer does in <= 2^21-ray batches (Renderer.cc:46,
-    RayGen.cc:124-142) — cut into block-cyclic shards (16 384-ray blocks dealt
-    round-robin to the ranks), each traced in <= 2^21-ray launches with no
-    collective; T_n = max over ranks. T_1 is measured in the same run (rank 0
+    RayGen.cc:124-142) — cut into block-cyclic shards (4 096-ray blocks dealt
+    round-robin to the ranks; --strong-balance 1 deals them by live-ray count),
+    each traced in <= 2^21-ray launches with no collective; T_n = max over ranks. T_1 is measured in the same run (rank 0
     traces the whole buffer alone), eta(n) = T_1 / (n T_n), with and without the
     RCCL gather of the {id, t} results to rank 0.
   * weak (the line's value at N = 1, BASELINE configs[1]; a sub-block at N > 1):
@@ -105,7 +105,7 @@ EXTRA_N1 = ["bunny-primary-640x480", "conference-ao-640x480", "sponza-diffuse-64
 # Strong-scaling config: scene, frame, samples per pixel, rays per launch.
 # min_launches: a shard is cut into at least this many launches (alternating over two streams).
 STRONG = {"name": "hairball-diffuse-1920x1080x8spp", "scene": "hairball", "w": 1920, "h": 1080, "spp": 8,
-          "max_batch": 1 << 21, "min_launches": 1, "block": 1 << 14, "streams": 2, "balance": True}
+          "max_batch": 1 << 21, "min_launches": 1, "block": 1 << 12, "streams": 2, "balance": False}
 STRONG_PROJECT = (2, 4, 8)   # N=1 only: rank counts whose per-rank shards are timed on the one GPU
 
 
@@ -891,8 +891,9 @@ def make_line(args, world, head, extras, strong, tracer_cfg):
         config = {"workload": strong["workload"], "scene": STRONG["scene"], "width": STRONG["w"],
                   "height": STRONG["h"], "samples_per_pixel": STRONG["spp"], "rays_total": strong["rays_traced"],
                   "ray_type": "diffuse", "rcp": args.rcp,
-                  "parallelism": (f"one RayBuffer in {world} block-cyclic shards ({STRONG['block']}-ray blocks "
-                                  f"dealt round-robin to the ranks), BVH replicated, no collective in the step"
+                  "parallelism": ((f"one RayBuffer in {world} shards of {STRONG['block']}-ray blocks "
+                                   + ("dealt by live-ray count" if STRONG["balance"] else "dealt round-robin (block-cyclic)")
+                                   + ", BVH replicated, no collective in the step")
                                   if STRONG["block"] > 0 else f"one RayBuffer in {world} contiguous shards"),
                   "launch_rays_max": STRONG["max_batch"]}
         steps = args.strong_steps
