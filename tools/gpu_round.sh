@@ -9,6 +9,7 @@
 #   profile=TAG     rocprofv3 kernel stats + PMC summaries of the bench workloads (PROF_WL overrides the list)
 #                                                                  -> gpurun_out/profiles/TAG_*
 #   readme          every README cell tuned, measured and checked  -> gpurun_out/readme_table.md
+#   pipe=W          vector-memory / VALU pipeline counters of workload W (4 PMC passes) -> gpurun_out/pipe_W.txt
 #   timeline=W      per-ray start / tail entry / end of workload W (MRT_TAIL_TIMELINE variant library)
 # Usage: bash tools/gpu_round.sh test smoke bench      (gpurun -- 'bash tools/gpu_round.sh ...')
 set -o pipefail
@@ -56,6 +57,12 @@ for step in "$@"; do
       timeout -k 10 900 python -u tools/readme_table.py --tune-db $O/tuned_schedules_all.json > $O/readme_table.log 2>&1 \
         || fail "readme table" $O/readme_table.log
       cat $O/readme_table.md ;;
+    pipe)
+      P="GRBM_GUI_ACTIVE TA_BUSY_avr TA_BUFFER_READ_WAVEFRONTS_sum;TD_TD_BUSY_sum TD_TC_STALL_sum GRBM_COUNT TCP_TOTAL_CACHE_ACCESSES_sum TCP_PENDING_STALL_CYCLES_sum"
+      P="$P;SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_LDS"
+      P="$P;SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL SQ_ACTIVE_INST_VMEM TA_ADDR_STALLED_BY_TC_CYCLES_sum TA_DATA_STALLED_BY_TC_CYCLES_sum GRBM_GUI_ACTIVE"
+      timeout -k 10 900 bash tools/pmc_pipe.sh $arg $O/pipe_$arg "$P" > $O/pipe_$arg.log 2>&1 || fail "pipe $arg" $O/pipe_$arg.log
+      python3 tools/pipe_summary.py $O/pipe_$arg > $O/pipe_$arg.txt && tail -12 $O/pipe_$arg.txt ;;
     timeline)
       MRT_LIB_DIR=$PWD/gpu-ray-tracing_amd/lib/variants/tailtl timeout -k 10 300 python -u tools/tail_timeline.py $arg \
         '{"tail_lanes": 0, "autotune": 0}' '{"tail_lanes": 16, "autotune": 0}' >> $O/tail_tl.txt 2>> $O/tail_tl.err || fail timeline $O/tail_tl.err
