@@ -64,7 +64,7 @@ def balance_blocks(weights, world: int) -> np.ndarray:
     return owners
 
 
-def shard_spans(n: int, world: int, rank: int, block: int = 0, owners=None) -> list[tuple[int, int]]:
+def shard_spans(n: int, world: int, rank: int, block: int = 0, owners=None, priority=None) -> list[tuple[int, int]]:
     """The ray ranges of `rank`'s shard of n rays. block = 0: one contiguous range
     (shard_range). block > 0: block-cyclic — the buffer cut into block-ray blocks,
     block i to rank i % world — so every shard draws from the whole frame. A
@@ -72,17 +72,29 @@ def shard_spans(n: int, world: int, rank: int, block: int = 0, owners=None) -> l
     RayGenKernels.cu:117-227), so contiguous shards are image regions of unequal
     cost: on the hairball 1920x1080x8spp buffer the 8 contiguous shards took
     0.59-1.12 ms on one MI355X, which caps eta(8) at 0.54. owners (block > 0):
-    block i to rank owners[i] instead (balance_blocks), adjacent blocks merged."""
-    if block <= 0 or world == 1:
+    block i to rank owners[i] instead (balance_blocks). priority (block > 0, one
+    value per block, e.g. block_weights): the rank's blocks in decreasing priority
+    (ties in frame order) instead of frame order, so a launch that deals its rays in
+    order starts its costly blocks first and ends on the cheap ones (with world = 1:
+    the whole buffer reordered). Blocks adjacent in the result are merged."""
+    nblocks = -(-n // block) if block > 0 else 0
+    if block <= 0 or (world == 1 and priority is None):
         lo, hi = shard_range(n, world, rank)
         return [(lo, hi)] if hi > lo else []
-    if owners is None:
-        return [(a, min(n, a + block)) for a in range(rank * block, n, world * block)]
-    owners = np.asarray(owners)
-    if len(owners) != -(-n // block):
-        raise ValueError(f"shard_spans: {len(owners)} block owners for {-(-n // block)} blocks of {block} rays")
+    if owners is not None:
+        owners = np.asarray(owners)
+        if len(owners) != nblocks:
+            raise ValueError(f"shard_spans: {len(owners)} block owners for {nblocks} blocks of {block} rays")
+        mine = np.flatnonzero(owners == rank)
+    else:
+        mine = np.arange(rank, nblocks, world)
+    if priority is not None:
+        pr = np.asarray(priority.cpu() if isinstance(priority, torch.Tensor) else priority)
+        if len(pr) != nblocks:
+            raise ValueError(f"shard_spans: {len(pr)} block priorities for {nblocks} blocks of {block} rays")
+        mine = mine[np.argsort(-pr[mine], kind="stable")]
     spans: list[tuple[int, int]] = []
-    for i in np.flatnonzero(owners == rank):
+    for i in mine:
         a, b = int(i) * block, min(n, (int(i) + 1) * block)
         if spans and spans[-1][1] == a:
             spans[-1] = (spans[-1][0], b)
@@ -168,21 +180,22 @@ def shard_launches(lo: int, hi: int, max_rays: int, min_launches: int = 1):
 
 
 def trace_shard(tracer, rays, world: int, rank: int, max_rays: int = 1 << 21, exact_rcp: bool = True,
-                stream=None, block: int = 0, owners=None):
+                stream=None, block: int = 0, owners=None, priority=None):
     """Strong-scaling step of one rank: trace its shard of the RayBuffer `rays`
     (every rank holds the same buffer) in launches of at most max_rays rays,
     stream-ordered. block = 0: the contiguous shard, results written in place;
     returns (lo, hi). block > 0: the block-cyclic shard, gathered into a local
     RayBuffer first; returns that buffer (its results are the shard's, in
     shard_spans order — what gather_results(..., block=block, owners=owners)
-    expects). owners: balance_blocks' deal of the blocks, or None (cyclic)."""
-    if block <= 0:
+    expects). owners: balance_blocks' deal of the blocks, or None (cyclic);
+    priority: the order of the blocks within the shard (shard_spans)."""
+    if block <= 0 or (world == 1 and priority is None):
         lo, hi = shard_range(rays.size, world, rank)
         for a, b in shard_launches(lo, hi, max_rays):
             tracer.trace_async(rays.view(a, b), exact_rcp=exact_rcp, stream=stream)
         return lo, hi
     from .tracer import RayBuffer
-    local = RayBuffer(local_rays(rays.rays, shard_spans(rays.size, world, rank, block, owners)),
+    local = RayBuffer(local_rays(rays.rays, shard_spans(rays.size, world, rank, block, owners, priority)),
                       rays.need_closest_hit)
     if stream is not None:
         # the local buffer was built on the current stream: the launches on `stream` wait for it
@@ -192,7 +205,7 @@ def trace_shard(tracer, rays, world: int, rank: int, max_rays: int = 1 << 21, ex
     return local
 
 
-def gather_results(local: torch.Tensor, n_total: int, dst: int = 0, block: int = 0, owners=None):
+def gather_results(local: torch.Tensor, n_total: int, dst: int = 0, block: int = 0, owners=None, priority=None):
     """Gather every rank's RayResult shard (int32 [k, 4], the shard's rays in
     shard_spans order) to rank `dst` in ray order with point-to-point send/recv
     (RCCL has no gather primitive; the root receives from all peers at once over
@@ -205,7 +218,7 @@ def gather_results(local: torch.Tensor, n_total: int, dst: int = 0, block: int =
                         f"{tuple(local.shape)}")
     if dist.get_backend() == "nccl" and not _on_device(local):
         raise ValueError("gather_results: RCCL (nccl) moves device tensors; got a " + local.device.type + " tensor")
-    mine = sum(b - a for a, b in shard_spans(n_total, world, rank, block, owners))
+    mine = sum(b - a for a, b in shard_spans(n_total, world, rank, block, owners, priority))
     if local.shape[0] != mine:
         raise ValueError(f"gather_results: rank {rank} holds {local.shape[0]} results, its shard of {n_total} "
                          f"rays has {mine}")
@@ -217,7 +230,7 @@ def gather_results(local: torch.Tensor, n_total: int, dst: int = 0, block: int =
     full = torch.empty((n_total, 2), dtype=torch.int32, device=local.device)
     reqs, scatter = [], []
     for r in range(world):
-        spans = shard_spans(n_total, world, r, block, owners)
+        spans = shard_spans(n_total, world, r, block, owners, priority)
         count = sum(b - a for a, b in spans)
         if count == 0:
             continue

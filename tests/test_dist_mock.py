@@ -229,3 +229,32 @@ def test_gather_results_with_a_weighted_deal(fake, world, block):
     assert torch.equal(out[0], full_ref[:, :2])
     with pytest.raises(ValueError, match="block owners"):
         D.shard_spans(n, world, 0, block, owners[:-1])
+
+
+@pytest.mark.parametrize("world,block,balanced", [(1, 1000, False), (2, 1000, False), (8, 4096, True), (3, 777, False)])
+def test_priority_orders_blocks_and_gathers_back(fake, world, block, balanced):
+    """shard_spans(..., priority=w): each rank's blocks in decreasing w (ties in
+    frame order), every ray still in exactly one shard, and gather_results puts
+    the results back in ray order (nccl branch)."""
+    n = 100_003
+    nblocks = -(-n // block)
+    rng = np.random.default_rng(block)
+    w = rng.integers(0, 5, nblocks)
+    owners = D.balance_blocks(w, world) if balanced else None
+    seen = torch.zeros(n, dtype=torch.int32)
+    for r in range(world):
+        spans = D.shard_spans(n, world, r, block, owners, w)
+        firsts = [a // block for a, _ in spans]
+        assert all(w[x] >= w[y] for x, y in zip(firsts, firsts[1:]))
+        seen[D.spans_index(spans)] += 1
+    assert bool((seen == 1).all())
+    full_ref = results_for(n)
+    f = fake(world)
+
+    def rank_fn(r):
+        idx = D.spans_index(D.shard_spans(n, world, r, block, owners, w))
+        return D.gather_results(full_ref[idx].contiguous(), n, dst=0, block=block, owners=owners, priority=w)
+    out = f.run(rank_fn)
+    assert torch.equal(out[0], full_ref[:, :2])
+    with pytest.raises(ValueError, match="block priorities"):
+        D.shard_spans(n, world, 0, block, owners, w[:-1])

@@ -42,10 +42,13 @@ def main():
     r.begin_frame(cam, 1920, 1080)
     big = torch.cat([b.rays for b, _ in r.batches()])
     n = big.shape[0]
-    owners = balance_blocks(block_weights(big, block), world) if balance else None
+    weights = block_weights(big, block)
+    owners = balance_blocks(weights, world) if balance else None
+    prio = weights if int(os.environ.get("ORDER", "0")) else None   # costly (live) blocks first in each shard
     shards = []
     for k in range(world):
-        rb = RayBuffer(local_rays(big, shard_spans(n, world, k, block, owners)).contiguous(), need_closest_hit=True)
+        rb = RayBuffer(local_rays(big, shard_spans(n, world, k, block, owners, prio)).contiguous(),
+                       need_closest_hit=True)
         shards.append((k, rb, int((rb.rays[:, 7] >= 0).sum())))
     torch.cuda.synchronize()
     if os.environ.get("STATS"):
@@ -57,7 +60,7 @@ def main():
                   f"nodes/live {st[0] / max(1, live):.2f}", flush=True)
     import time
     from mrt.dist import shard_launches
-    whole = RayBuffer(big, need_closest_hit=True)
+    whole = RayBuffer(local_rays(big, shard_spans(n, 1, 0, block, None, prio)).contiguous(), need_closest_hit=True)
     streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
     import json
     for item in filter(None, os.environ.get("EXTRA_SCHEDS", "").split(";")):
