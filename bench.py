@@ -19,9 +19,11 @@ replicated). Two scalings are measured in every run:
   * strong (BASELINE configs[4]; the line's value at N > 1): ONE
     fixed RayBuffer — hairball diffuse 1920x1080 x 8 spp = 16.6 M rays, generated
     as the reference's Renderer does in <= 2^21-ray batches (Renderer.cc:46,
-    RayGen.cc:124-142) — cut into block-cyclic shards (4 096-ray blocks dealt
+    RayGen.cc:124-142) — cut into block-cyclic shards (1 024-ray blocks dealt
     round-robin to the ranks; --strong-balance 1 deals them by live-ray count),
-    each traced in <= 2^21-ray launches with no collective; T_n = max over ranks. T_1 is measured in the same run (rank 0
+    each shard's blocks ordered live rays first (--strong-order; T_1's buffer
+    too), each traced in <= 2^21-ray launches with no collective; T_n = max over
+    ranks. T_1 is measured in the same run (rank 0
     traces the whole buffer alone), eta(n) = T_1 / (n T_n), with and without the
     RCCL gather of the {id, t} results to rank 0.
   * weak (the line's value at N = 1, BASELINE configs[1]; a sub-block at N > 1):
@@ -105,7 +107,8 @@ EXTRA_N1 = ["bunny-primary-640x480", "conference-ao-640x480", "sponza-diffuse-64
 # Strong-scaling config: scene, frame, samples per pixel, rays per launch.
 # min_launches: a shard is cut into at least this many launches (alternating over two streams).
 STRONG = {"name": "hairball-diffuse-1920x1080x8spp", "scene": "hairball", "w": 1920, "h": 1080, "spp": 8,
-          "max_batch": 1 << 21, "min_launches": 1, "block": 1 << 12, "streams": 2, "balance": False}
+          "max_batch": 1 << 21, "min_launches": 1, "block": 1 << 10, "streams": 2, "balance": False,
+          "order": True}
 STRONG_PROJECT = (2, 4, 8)   # N=1 only: rank counts whose per-rank shards are timed on the one GPU
 
 
@@ -597,7 +600,7 @@ def exploration_cost(tracer, gbvh, rb, exact, max_launches=200):
 
 # cfg.autotune candidates (csrc/mrt_api.cpp tune_candidate)
 SCHEDULES = {0: "static rounds, 20 waves/CU", 1: "static rounds, 8 waves/CU",
-             2: "8 per-XCD queues of 4096-ray blocks, 5 % shared, refill at 48, 20 waves/CU",
+             2: "8 per-XCD queues of 8192-ray blocks, 5 % shared, refill at 48, 20 waves/CU",
              3: "global queue, refill at 48, 16 waves/CU", 4: "global queue, refill at 48, 12 waves/CU",
              5: "static rounds, 16 waves/CU", 6: "static rounds, 12 waves/CU",
              7: "global queue, refill at 48, 20 waves/CU"}
@@ -706,7 +709,8 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
     whole buffer alone, same run; then the {id, t} gather to rank 0, checked
     against the single-GPU results."""
     import torch
-    from mrt.dist import balance_blocks, block_weights, gather_results, local_rays, shard_launches, shard_spans
+    from mrt.dist import (balance_blocks, block_weights, gather_results, local_rays, shard_launches, shard_spans,
+                          spans_index)
     from mrt.raygen import RAY_DIFFUSE
     from mrt.renderer import Renderer
     from mrt.tracer import RayBuffer
@@ -725,11 +729,16 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
 
     # Blocks dealt by live-ray count (balance_blocks) or cyclically: every rank
     # computes the same deal from the buffer's tmax column (one reduction).
-    weights = block_weights(big.rays, cfg["block"]) if cfg["balance"] and cfg["block"] > 0 else None
+    # Blocks dealt by live-ray count (balance_blocks) or cyclically, and within a shard
+    # in frame order or costly (live) blocks first (order): every rank computes the same
+    # deal from the buffer's tmax column (one reduction).
+    weights = (block_weights(big.rays, cfg["block"]) if (cfg["balance"] or cfg["order"]) and cfg["block"] > 0
+               else None)
+    prio = weights if cfg["order"] else None
     deals = {}
 
     def owners_for(k):
-        if weights is None or k == 1:
+        if weights is None or k == 1 or not cfg["balance"]:
             return None
         if k not in deals:
             deals[k] = balance_blocks(weights, k)
@@ -738,10 +747,12 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
     def shard_buffer(k, rk):
         # the shard as one contiguous RayBuffer (built before the timed region: a
         # rank generating its own rays would produce it in this order directly)
-        return RayBuffer(local_rays(big.rays, shard_spans(n, k, rk, cfg["block"], owners_for(k))),
+        return RayBuffer(local_rays(big.rays, shard_spans(n, k, rk, cfg["block"], owners_for(k), prio)),
                          need_closest_hit=True)
 
-    local = big if world == 1 else shard_buffer(world, rank)
+    if prio is not None:   # T_1's buffer in the same block order (its results are gathered back the same way)
+        big_local = shard_buffer(1, 0)
+    local = (big_local if prio is not None else big) if world == 1 else shard_buffer(world, rank)
     torch.cuda.synchronize()
     # The shard's <= 2^21-ray launches are independent batches: they alternate
     # between two streams (each stream has its own trace scratch), so one
@@ -772,20 +783,26 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
     # gather of this shard's {id, t} to rank 0 (RCCL point-to-point; gloo: via host),
     # after one untimed gather (RCCL creates its point-to-point communicators on first use)
     if world > 1:
-        gather_results(local.results if DIST_BACKEND == "nccl" else local.results.cpu(), n, block=cfg["block"], owners=owners_for(world))
+        gather_results(local.results if DIST_BACKEND == "nccl" else local.results.cpu(), n, block=cfg["block"],
+                       owners=owners_for(world), priority=prio)
     torch.cuda.synchronize()
     barrier(world)
     t0 = time.perf_counter()
     res = local.results if DIST_BACKEND == "nccl" else local.results.cpu()
-    full = gather_results(res, n, block=cfg["block"], owners=owners_for(world)) if world > 1 else big.results[:, :2]
+    full = (gather_results(res, n, block=cfg["block"], owners=owners_for(world), priority=prio) if world > 1
+            else big.results[:, :2])
     torch.cuda.synchronize()
     gather_ms = reduce_over_ranks(1e3 * (time.perf_counter() - t0), world) if world > 1 else 0.0
     # T_1 in the same run: rank 0 alone over the whole buffer (the others wait)
     if world > 1:
         equal = None
         if rank == 0:
-            w1, _, _ = time_steps(shard_steps(big), steps, warmup, 1)
+            t1buf = big if prio is None else shard_buffer(1, 0)   # the same block order as the N = 1 run
+            w1, _, _ = time_steps(shard_steps(t1buf), steps, warmup, 1)
             t1 = w1 / steps * 1e3
+            if prio is not None:   # T_1's results back in ray order
+                idx1 = spans_index(shard_spans(n, 1, 0, cfg["block"], None, prio), t1buf.results.device)
+                big.results[idx1] = t1buf.results
             equal = bool(torch.equal(full.to(big.results.device), big.results[:, :2]))
         barrier(world)
         t1 = reduce_over_ranks(t1 if rank == 0 else 0.0, world)
@@ -816,8 +833,9 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
         "eta_with_gather": round(t1 / (world * (tn + gather_ms)), 4),
         "value": round(counted / (tn * 1e-3) / 1e6, 2), "value_with_gather": round(counted / ((tn + gather_ms) * 1e-3) / 1e6, 2),
         "gathered_equals_single_gpu": equal, "streams": len(streams), "min_launches": cfg["min_launches"],
-        "shards": ((f"{cfg['block']}-ray blocks dealt by live-ray count" if weights is not None
-                    else f"block-cyclic, {cfg['block']}-ray blocks") if cfg["block"] > 0 else "contiguous"),
+        "shards": (((f"{cfg['block']}-ray blocks dealt by live-ray count" if cfg["balance"]
+                     else f"block-cyclic, {cfg['block']}-ray blocks")
+                    + (", live blocks first" if cfg["order"] else "")) if cfg["block"] > 0 else "contiguous"),
         "projected_from_one_gpu": projected,
         "roofline": shard_roofline,
         "collective": f"{DIST_BACKEND} point-to-point gather of {n * 8} B to rank 0" if world > 1 else None,
@@ -893,6 +911,7 @@ def make_line(args, world, head, extras, strong, tracer_cfg):
                   "ray_type": "diffuse", "rcp": args.rcp,
                   "parallelism": ((f"one RayBuffer in {world} shards of {STRONG['block']}-ray blocks "
                                    + ("dealt by live-ray count" if STRONG["balance"] else "dealt round-robin (block-cyclic)")
+                                   + (", each shard's live blocks first" if STRONG["order"] else "")
                                    + ", BVH replicated, no collective in the step")
                                   if STRONG["block"] > 0 else f"one RayBuffer in {world} contiguous shards"),
                   "launch_rays_max": STRONG["max_batch"]}
@@ -951,6 +970,8 @@ def main():
                     help="block-cyclic shard block (rays); 0 = contiguous shards")
     ap.add_argument("--strong-balance", type=int, default=int(STRONG["balance"]), choices=[0, 1],
                     help="1: deal the shard blocks by live-ray count (mrt.dist.balance_blocks); 0: cyclically")
+    ap.add_argument("--strong-order", type=int, default=int(STRONG["order"]), choices=[0, 1],
+                    help="1: each shard's blocks in decreasing live-ray count (mrt.dist.shard_spans priority)")
     ap.add_argument("--strong-streams", type=int, default=STRONG["streams"], choices=[1, 2],
                     help="caller streams the strong-scaling launches alternate over")
     ap.add_argument("--strong-min-launches", type=int, default=STRONG["min_launches"],
@@ -1028,6 +1049,7 @@ def main():
         STRONG["block"] = max(0, args.strong_block)
         STRONG["streams"] = args.strong_streams
         STRONG["balance"] = bool(args.strong_balance)
+        STRONG["order"] = bool(args.strong_order)
         strong = strong_scaling(tracer, scenes, world, rank, args.strong_steps, 3, exact,
                                 with_roofline=args.scaling == "strong")
         log(f"[strong] {strong['workload']} n={world}: T1 {strong['t1_ms']} ms, Tn {strong['tn_ms']} ms, "

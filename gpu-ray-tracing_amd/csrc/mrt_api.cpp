@@ -481,7 +481,7 @@ int refresh_wide(mrt_tracer* t) {
 // (mrt_tracer_tune_export / _import, mrt/tuned_schedules.json for the bench).
 constexpr int kMaxTuned = 64;   // batch sizes tuned per handle; others use the rule
 constexpr int64_t kTuneInherit = 32;   // a new batch size within 1/32 of a settled one takes its schedule
-constexpr int kXcdQueueBlock = 4096;   // candidate 2's per-XCD queue blocks (rays) and shared tail (%)
+constexpr int kXcdQueueBlock = 8192;   // candidate 2's per-XCD queue blocks (rays) and shared tail (%)
 constexpr int kXcdQueueShared = 5;
 
 mrt_launch_cfg tune_candidate(const mrt_launch_cfg& base, int c, int stage1) {
@@ -508,11 +508,12 @@ mrt_launch_cfg tune_candidate(const mrt_launch_cfg& base, int c, int stage1) {
     switch (c) {
         case 0: break;                                                      // static rounds, 20 waves/CU
         case 1: x.waves_per_cu = 8; break;                                  // static rounds, fewer waves
-        case 2:   // per-XCD queues of 4096-ray blocks dealt cyclically (every XCD samples the whole frame,
+        case 2:   // per-XCD queues of 8192-ray blocks dealt cyclically (every XCD samples the whole frame,
                   // its L2 holds its own blocks' nodes and triangles), the last 5 % in one shared queue,
                   // refills at 48 live lanes, 20 waves/CU: a multi-million-ray launch over a BVH above the
-                  // Infinity Cache (hairball 2 M rays: 0.630 -> 0.547 ms, fabric bytes 1.07 -> 0.74 GB;
-                  // profiles/round4_queue_ab.txt)
+                  // Infinity Cache (hairball 2 M rays: 0.630 -> 0.547 ms, fabric bytes 1.07 -> 0.74 GB at
+                  // 4096-ray blocks, profiles/round4_queue_ab.txt; 8192: 1.4 % faster again and the
+                  // strong-scaling shards' best, round4_order_sweep.txt)
             x.num_queues = 8;
             x.queue_block = kXcdQueueBlock;
             x.queue_shared = kXcdQueueShared;
