@@ -542,7 +542,7 @@ def roofline(name, alg_bytes_per_launch, kernel_ms, bvh_bytes, schedule, rcp="ex
     not clamped: SURVEY §8d). `served` prices what each level actually moved against its
     own ceiling (L1->L2 requests / 34.5 TB/s; fabric / 8.6 TB/s, the Infinity Cache's
     random-row rate) and names the larger as `binding_level`. The cited profile must
-    have run the timed schedule (autotune candidate, grid, queues) or none is cited."""
+    have run the timed schedule (autotune candidate and its name, grid, queues) or none is cited."""
     t = kernel_ms * 1e-3
     alg = alg_bytes_per_launch / t / 1e9
     out = {"bound": "hbm", "achieved": round(alg, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -552,7 +552,8 @@ def roofline(name, alg_bytes_per_launch, kernel_ms, bvh_bytes, schedule, rcp="ex
            "bvh_bytes": int(bvh_bytes), "bvh_exceeds_mall": bvh_bytes > MALL_BYTES}
     if alg > HBM_PEAK_GBS:
         out["note"] = "algorithmic rate above the HBM peak: the BVH is cache-resident (L1/L2 hits)"
-    want = {k: schedule.get(k) for k in ("autotune_candidate", "grid_waves", "num_queues", "fetch_threshold")}
+    # the schedule's name too: it spells out what the candidate number means in this build (queue blocks, ...)
+    want = {k: schedule.get(k) for k in ("autotune_candidate", "name", "grid_waves", "num_queues", "fetch_threshold")}
     profs = pmc_profile(name, rcp)
     prof = next((p for p in profs if {k: (p.get("schedule") or {}).get(k) for k in want} == want), None)
     if prof is None:
