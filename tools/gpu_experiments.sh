@@ -1,0 +1,83 @@
+#!/bin/bash
+# Round-4 experiments, one GPU box, by name (each step bounded; the first failure ends the session):
+#   done_event   back-to-back cost of a completion event per launch: lib vs variants/doneev
+#                (tools/build_variant.sh doneev "-DMRT_DONE_EVENT")          -> profiles/round4_done_event_ab.txt
+#   queue        rule vs per-XCD block-cyclic queue forms, times + fabric bytes (tools/pmc_configs.sh)
+#                                                                            -> profiles/round4_queue_*.txt
+#   wideq        quantized 64-B wide nodes vs exact on the hairball frames   -> profiles/round4_wideq_ab.txt
+#   strong_launches   strong-scaling shards cut into 1..4 launches (bench --strong-min-launches)
+#   strong_blocks     block size x balance of the strong-scaling shards (BLOCKS, BALANCE)
+#   shard_sweep  the 8 shards under per-XCD queue variants, frame order     -> tools/strong_diag.py
+#   order        live blocks first: dist block x balance x queue block      -> profiles/round4_order_sweep.txt
+#   order2       live blocks first: ordering granularity x shared-queue share -> profiles/round4_order_sweep2.txt
+# Usage: gpurun -- 'bash tools/gpu_experiments.sh order order2'
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out; export TMPDIR=/tmp
+O=gpurun_out
+fail() { echo "$1 failed"; tail -20 "$2"; exit 1; }
+Q8='"autotune":0,"num_queues":8,"fetch_threshold":48,"waves_per_cu":20'
+for exp in "$@"; do
+  case $exp in
+    done_event)
+      timeout -k 10 600 python -u tools/ab.py --rounds 7 --launches 30 --workload conference-ao-640x480 --workload mori-ao-640x480 \
+        --workload bunny-primary-640x480 --workload bunny-primary-1024x768 --workload hairball-diffuse-1920x1080 \
+        --variant 'lib:{"saved":1}' --variant 'lib/variants/doneev:{"saved":1}' --variant 'lib:{"autotune":0}' \
+        --variant 'lib/variants/doneev:{"autotune":0}' > $O/ab_done.txt 2> $O/ab_done.err || fail ab $O/ab_done.err
+      cat $O/ab_done.txt ;;
+    queue)
+      CFGS=('{"autotune":0}' "{$Q8,\"queue_shared\":10,\"queue_block\":16384}" "{$Q8,\"queue_shared\":5,\"queue_block\":4096}"
+            "{$Q8,\"queue_shared\":5,\"queue_block\":8192}" "{$Q8,\"queue_shared\":10,\"queue_block\":65536}")
+      V=""; for c in "${CFGS[@]}"; do V="$V --variant lib:$c"; done
+      timeout -k 10 900 python -u tools/ab.py --rounds 5 --launches 20 --workload hairball-diffuse-1920x1080 --workload hairball-diffuse-640x480 \
+        --workload bunny-primary-1024x768 --workload mori-ao-640x480 --workload conference-ao-640x480 $V > $O/ab_q.txt 2> $O/ab_q.err || fail ab $O/ab_q.err
+      cat $O/ab_q.txt
+      timeout -k 10 900 bash tools/pmc_configs.sh hairball-diffuse-1920x1080 "${CFGS[@]}" > $O/pmc_cfg.txt 2>&1 || fail pmc $O/pmc_cfg.txt
+      cat $O/pmc_cfg.txt ;;
+    wideq)
+      X="$Q8,\"spec_slack\":6,\"queue_shared\":5,\"queue_block\":8192"
+      timeout -k 10 500 python -u tools/ab.py --rounds 7 --launches 30 --workload hairball-diffuse-1920x1080 --workload hairball-diffuse-640x480 \
+        --workload hairball-primary-1024x768 --variant "lib:{$X}" --variant "lib:{$X,\"wide\":2}" --variant 'lib:{"autotune":0}' \
+        --variant 'lib:{"autotune":0,"wide":2}' > $O/ab_wideq.txt 2> $O/ab_wideq.err || fail ab $O/ab_wideq.err
+      cat $O/ab_wideq.txt ;;
+    strong_launches)
+      for ML in 1 2 3 4; do
+        timeout -k 10 300 python bench.py --no-extra --no-cpu --no-fast --no-explore --steps 20 --strong-min-launches $ML \
+          --detail-out $O/strong_ml$ML.json > $O/strong_ml$ML.out 2> $O/strong_ml$ML.err || fail "ml $ML" $O/strong_ml$ML.err
+        echo "min_launches $ML: $(grep strong $O/strong_ml$ML.err)"
+      done ;;
+    strong_blocks)
+      for BAL in ${BALANCE:-1 0}; do for B in ${BLOCKS:-16384 4096 1024 256}; do
+        T=b${B}_bal$BAL
+        timeout -k 10 300 python bench.py --no-extra --no-cpu --no-fast --no-explore --steps 20 --strong-steps 20 --strong-block $B \
+          --strong-balance $BAL --detail-out $O/strong_$T.json > $O/strong_$T.out 2> $O/strong_$T.err || fail $T $O/strong_$T.err
+        python3 -c "
+import json; d=json.load(open('$O/strong_$T.json'))['strong']
+print('block $B balance $BAL T1', d['t1_ms'], 'one-stream', d.get('one_stream_ms'), {k: (v['eta'], [round(x,3) for x in v['shard_ms']]) for k, v in d['projected_from_one_gpu'].items()})"
+      done; done ;;
+    shard_sweep)
+      EXTRA_SCHEDS="sh5b4096={$Q8,\"queue_shared\":5,\"queue_block\":4096};sh15b4096={$Q8,\"queue_shared\":15,\"queue_block\":4096};sh30b4096={$Q8,\"queue_shared\":30,\"queue_block\":4096};sh5b16384={$Q8,\"queue_shared\":5,\"queue_block\":16384}" \
+      SCHEDS=sh5b4096,sh15b4096,sh30b4096,sh5b16384 ORDERS=fwd REPS=7 \
+        timeout -k 10 600 python -u tools/strong_diag.py > $O/shard_sweep.txt 2> $O/shard_sweep.err || fail diag $O/shard_sweep.err
+      cat $O/shard_sweep.txt ;;
+    order)
+      B="$Q8,\"spec_slack\":6,\"queue_shared\":5"
+      timeout -k 10 400 python -u tools/ab.py --rounds 7 --launches 30 --workload hairball-diffuse-1920x1080 \
+        --variant "lib:{$B,\"queue_block\":4096}" --variant "lib:{$B,\"queue_block\":8192}" --variant "lib:{$B,\"queue_block\":16384}" \
+        > $O/ab_qblock.txt 2> $O/ab_qblock.err || fail ab $O/ab_qblock.err
+      cat $O/ab_qblock.txt
+      for BL in 1024 4096; do for BAL in 0 1; do
+        EXTRA_SCHEDS="x4096={$B,\"queue_block\":4096};x8192={$B,\"queue_block\":8192};x16384={$B,\"queue_block\":16384}" \
+        SCHEDS=x4096,x8192,x16384 ORDERS=fwd REPS=7 ORDER=1 BLOCK=$BL BALANCE=$BAL \
+          timeout -k 10 300 python -u tools/strong_diag.py > $O/order_b${BL}_bal$BAL.txt 2> $O/order_b${BL}_bal$BAL.err || fail diag $O/order_b${BL}_bal$BAL.err
+      done; done ;;
+    order2)
+      B="$Q8,\"spec_slack\":6"
+      for BL in 256 1024; do
+        EXTRA_SCHEDS="q8s5={$B,\"queue_block\":8192,\"queue_shared\":5};q8s10={$B,\"queue_block\":8192,\"queue_shared\":10};q8s20={$B,\"queue_block\":8192,\"queue_shared\":20};q16s10={$B,\"queue_block\":16384,\"queue_shared\":10}" \
+        SCHEDS=q8s5,q8s10,q8s20,q16s10 ORDERS=fwd REPS=7 ORDER=1 BLOCK=$BL \
+          timeout -k 10 300 python -u tools/strong_diag.py > $O/order2_b$BL.txt 2> $O/order2_b$BL.err || fail diag $O/order2_b$BL.err
+      done ;;
+    *) echo "unknown experiment $exp"; exit 2 ;;
+  esac
+done
