@@ -51,6 +51,35 @@ def main():
                        need_closest_hit=True)
         shards.append((k, rb, int((rb.rays[:, 7] >= 0).sum())))
     torch.cuda.synchronize()
+    if os.environ.get("TIMELINE"):
+        # per-ray {start, end, tail entry, iterations} of shard 0 (needs MRT_LIB_DIR = a -DMRT_TAIL_TIMELINE build)
+        import numpy as np
+        name = os.environ.get("SCHEDS", "x8192").split(",")[0]
+        for item in filter(None, os.environ.get("EXTRA_SCHEDS", "").split(";")):
+            nm, cfg = item.split("=", 1)
+            SCHEDULES[nm] = __import__("json").loads(cfg)
+        tracer.set_config(**SCHEDULES[name])
+        k, rb, live = shards[0]
+        for _ in range(3):
+            tracer.trace_batch(rb, exact_rcp=True)
+        st = None
+        for _ in range(3):
+            tracer.trace_batch(rb, exact_rcp=True, stats=True)
+            st = rb.stats.cpu().numpy().astype(np.int64)
+        t0 = st[:, 0].min()
+        start, end = (st[:, 0] - t0) * 0.01, (st[:, 1] - t0) * 0.01
+        dry = start.max()
+        liv = rb.rays[:, 7].cpu().numpy() >= 0
+        print(f"timeline shard {k} ({name}): last ray ends {end.max():.1f} us; first-round starts by "
+              f"{np.percentile(start, 1):.1f}..{np.percentile(start[:327680], 99):.1f} us; "
+              + " ".join(f"{q}%:{np.percentile(end, q):.1f}" for q in (50, 90, 99, 99.9)), flush=True)
+        print(f"   last fetch {dry:.1f} us; live rays in flight then {int(((start <= dry) & (end > dry) & liv).sum())}; "
+              f"in flight at +10/+25/+50 us: " + " ".join(str(int(((start <= dry + d) & (end > dry + d)).sum()))
+                                                       for d in (10, 25, 50)), flush=True)
+        last_live_start = start[liv].max()
+        print(f"   last live ray fetched at {last_live_start:.1f} us; live rays done by then "
+              f"{100.0 * (end[liv] <= last_live_start).mean():.1f} %", flush=True)
+        return
     if os.environ.get("STATS"):
         # the shards' traversal work: node visits and triangle tests per shard (STATS variant)
         for k, rb, live in shards:
