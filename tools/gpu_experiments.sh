@@ -10,6 +10,9 @@
 #   shard_sweep  the 8 shards under per-XCD queue variants, frame order     -> tools/strong_diag.py
 #   order        live blocks first: dist block x balance x queue block      -> profiles/round4_order_sweep.txt
 #   order2       live blocks first: ordering granularity x shared-queue share -> profiles/round4_order_sweep2.txt
+#   shard_sched  live blocks first, 1024-ray blocks: the shards under slack / waves / tail / lane-group variants
+#   ao_knobs     Mori / Fairy AO under launch knobs the autotuner does not explore
+#   timeline_shard  per-ray timeline of shard 0, live first vs frame order (variants/tailtl build)
 # Usage: gpurun -- 'bash tools/gpu_experiments.sh order order2'
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -78,6 +81,28 @@ print('block $B balance $BAL T1', d['t1_ms'], 'one-stream', d.get('one_stream_ms
         SCHEDS=q8s5,q8s10,q8s20,q16s10 ORDERS=fwd REPS=7 ORDER=1 BLOCK=$BL \
           timeout -k 10 300 python -u tools/strong_diag.py > $O/order2_b$BL.txt 2> $O/order2_b$BL.err || fail diag $O/order2_b$BL.err
       done ;;
+    shard_sched)
+      B="$Q8,\"queue_shared\":5"
+      EXTRA_SCHEDS="s8k6={$B,\"queue_block\":8192,\"spec_slack\":6};s8k4={$B,\"queue_block\":8192,\"spec_slack\":4};s8k2={$B,\"queue_block\":8192};s16k6={$B,\"queue_block\":16384,\"spec_slack\":6};s16k4={$B,\"queue_block\":16384,\"spec_slack\":4};s8k6w16={$B,\"queue_block\":8192,\"spec_slack\":6,\"waves_per_cu\":16};s8k6t0={$B,\"queue_block\":8192,\"spec_slack\":6,\"tail_lanes\":0};s8k6lg={$B,\"queue_block\":8192,\"spec_slack\":6,\"lane_groups\":16}" \
+      SCHEDS=s8k6,s8k4,s8k2,s16k6,s16k4,s8k6w16,s8k6t0,s8k6lg ORDERS=fwd REPS=7 ORDER=1 BLOCK=1024 \
+        timeout -k 10 600 python -u tools/strong_diag.py > $O/shard_sched.txt 2> $O/shard_sched.err || fail diag $O/shard_sched.err ;;
+    timeline_shard)
+      X="$Q8,\"spec_slack\":6,\"queue_shared\":5,\"queue_block\":8192"
+      for ORD in 1 0; do
+        MRT_LIB_DIR=$PWD/gpu-ray-tracing_amd/lib/variants/tailtl EXTRA_SCHEDS="x8192={$X}" SCHEDS=x8192 BLOCK=1024 TIMELINE=1 ORDER=$ORD \
+          timeout -k 10 300 python -u tools/strong_diag.py > $O/tlshard$ORD.txt 2> $O/tlshard$ORD.err || fail timeline $O/tlshard$ORD.err
+        cat $O/tlshard$ORD.txt
+      done ;;
+    ao_knobs)
+      V=""
+      for c in '{"autotune":0}' '{"autotune":0,"spec_slack":4}' '{"autotune":0,"tail_lanes":8}' '{"autotune":0,"tail_lanes":4}' \
+               '{"autotune":0,"lane_groups":4}' '{"autotune":0,"lane_groups":2}' '{"autotune":0,"lds_stack":8}' \
+               '{"autotune":0,"waves_per_cu":16}' '{"autotune":0,"waves_per_cu":16,"lane_groups":4}' '{"autotune":0,"spec_slack":8}'; do
+        V="$V --variant lib:$c"
+      done
+      timeout -k 10 600 python -u tools/ab.py --rounds 7 --launches 30 --workload mori-ao-640x480 --workload fairy-ao-640x480 $V \
+        > $O/ab_ao.txt 2> $O/ab_ao.err || fail ab $O/ab_ao.err
+      cat $O/ab_ao.txt ;;
     *) echo "unknown experiment $exp"; exit 2 ;;
   esac
 done
