@@ -601,7 +601,7 @@ def exploration_cost(tracer, gbvh, rb, exact, max_launches=200):
 
 # cfg.autotune candidates (csrc/mrt_api.cpp tune_candidate)
 SCHEDULES = {0: "static rounds, 20 waves/CU", 1: "static rounds, 8 waves/CU",
-             2: "8 per-XCD queues of 8192-ray blocks, 5 % shared, refill at 48, 20 waves/CU",
+             2: "8 per-XCD queues of 8192-ray blocks, refill at 56, 20 waves/CU",
              3: "global queue, refill at 48, 16 waves/CU", 4: "global queue, refill at 48, 12 waves/CU",
              5: "static rounds, 16 waves/CU", 6: "static rounds, 12 waves/CU",
              7: "global queue, refill at 48, 20 waves/CU"}

@@ -481,8 +481,13 @@ int refresh_wide(mrt_tracer* t) {
 // (mrt_tracer_tune_export / _import, mrt/tuned_schedules.json for the bench).
 constexpr int kMaxTuned = 64;   // batch sizes tuned per handle; others use the rule
 constexpr int64_t kTuneInherit = 32;   // a new batch size within 1/32 of a settled one takes its schedule
-constexpr int kXcdQueueBlock = 8192;   // candidate 2's per-XCD queue blocks (rays) and shared tail (%)
-constexpr int kXcdQueueShared = 5;
+// Candidate 2's per-XCD queue blocks (rays), shared tail (%) and refill threshold. No shared tail: on a
+// frame in pixel order it bought 0.6 %, and on a buffer ordered costly-first (the strong-scaling shards,
+// mrt.dist priority) its last rays retire at once and every XCD's waves then contend for one queue head
+// (T_1 3.44 -> 3.20 ms, 8-rank shards 0.490 -> 0.445 ms without it; profiles/round4_shared_queue.txt).
+constexpr int kXcdQueueBlock = 8192;
+constexpr int kXcdQueueShared = 0;
+constexpr int kXcdQueueThreshold = 56;
 
 mrt_launch_cfg tune_candidate(const mrt_launch_cfg& base, int c, int stage1) {
     if (c >= TuneState::kSchedules) {
@@ -509,15 +514,15 @@ mrt_launch_cfg tune_candidate(const mrt_launch_cfg& base, int c, int stage1) {
         case 0: break;                                                      // static rounds, 20 waves/CU
         case 1: x.waves_per_cu = 8; break;                                  // static rounds, fewer waves
         case 2:   // per-XCD queues of 8192-ray blocks dealt cyclically (every XCD samples the whole frame,
-                  // its L2 holds its own blocks' nodes and triangles), the last 5 % in one shared queue,
-                  // refills at 48 live lanes, 20 waves/CU: a multi-million-ray launch over a BVH above the
+                  // its L2 holds its own blocks' nodes and triangles), no shared tail queue,
+                  // refills at 56 live lanes, 20 waves/CU: a multi-million-ray launch over a BVH above the
                   // Infinity Cache (hairball 2 M rays: 0.630 -> 0.547 ms, fabric bytes 1.07 -> 0.74 GB at
                   // 4096-ray blocks, profiles/round4_queue_ab.txt; 8192: 1.4 % faster again and the
                   // strong-scaling shards' best, round4_order_sweep.txt)
             x.num_queues = 8;
             x.queue_block = kXcdQueueBlock;
             x.queue_shared = kXcdQueueShared;
-            x.fetch_threshold = kBigQueueThreshold;
+            x.fetch_threshold = kXcdQueueThreshold;
             x.waves_per_cu = kStridedWaves;
             break;
         case 3: x.num_queues = 1; x.fetch_threshold = kBigQueueThreshold; x.waves_per_cu = kBigQueueWaves; break;   // global queue

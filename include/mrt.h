@@ -163,7 +163,7 @@ typedef struct mrt_tuned_schedule {
     int32_t candidate;
     int32_t version;           /* MRT_TUNE_VERSION when exported; others are refused on import */
 } mrt_tuned_schedule;
-enum { MRT_TUNE_VERSION = 8 };
+enum { MRT_TUNE_VERSION = 9 };
 
 /* ---- handle API -------------------------------------------------------- */
 int  mrt_tracer_create(int device, mrt_tracer** out);

@@ -11,6 +11,8 @@
 #   order        live blocks first: dist block x balance x queue block      -> profiles/round4_order_sweep.txt
 #   order2       live blocks first: ordering granularity x shared-queue share -> profiles/round4_order_sweep2.txt
 #   shard_sched  live blocks first, 1024-ray blocks: the shards under slack / waves / tail / lane-group variants
+#   shard_knobs  live blocks first, 1024-ray blocks: shared share / static rounds / refill threshold / tail lanes
+#   shared_frame the shared-queue share on the 1 spp hairball frames and on ordered shards (0 / 2 / 5 %)
 #   ao_knobs     Mori / Fairy AO under launch knobs the autotuner does not explore
 #   timeline_shard  per-ray timeline of shard 0, live first vs frame order (variants/tailtl build)
 # Usage: gpurun -- 'bash tools/gpu_experiments.sh order order2'
@@ -93,6 +95,25 @@ print('block $B balance $BAL T1', d['t1_ms'], 'one-stream', d.get('one_stream_ms
           timeout -k 10 300 python -u tools/strong_diag.py > $O/tlshard$ORD.txt 2> $O/tlshard$ORD.err || fail timeline $O/tlshard$ORD.err
         cat $O/tlshard$ORD.txt
       done ;;
+    shard_knobs)
+      B="$Q8,\"queue_block\":8192,\"spec_slack\":6"
+      EXTRA_SCHEDS="base={$B,\"queue_shared\":5};sh2={$B,\"queue_shared\":2};sh0={$B,\"queue_shared\":0};sr2={$B,\"queue_shared\":5,\"static_rounds\":2};ft32={$B,\"queue_shared\":5,\"fetch_threshold\":32};ft56={$B,\"queue_shared\":5,\"fetch_threshold\":56};tl8={$B,\"queue_shared\":5,\"tail_lanes\":8}" \
+      SCHEDS=base,sh2,sh0,sr2,ft32,ft56,tl8 ORDERS=fwd REPS=7 ORDER=1 BLOCK=1024 \
+        timeout -k 10 600 python -u tools/strong_diag.py > $O/shard_knobs.txt 2> $O/shard_knobs.err || fail diag $O/shard_knobs.err ;;
+    shared_frame)
+      B="$Q8,\"spec_slack\":6"
+      V=""
+      for c in "{$B,\"queue_block\":8192,\"queue_shared\":5}" "{$B,\"queue_block\":8192,\"queue_shared\":2}" "{$B,\"queue_block\":8192,\"queue_shared\":0}" \
+               "{$B,\"queue_block\":4096,\"queue_shared\":0}" "{$B,\"queue_block\":16384,\"queue_shared\":0}" "{$B,\"queue_block\":8192,\"queue_shared\":0,\"fetch_threshold\":56}"; do
+        V="$V --variant lib:$c"
+      done
+      timeout -k 10 500 python -u tools/ab.py --rounds 7 --launches 30 --workload hairball-diffuse-1920x1080 --workload hairball-diffuse-640x480 $V \
+        > $O/ab_shared.txt 2> $O/ab_shared.err || fail ab $O/ab_shared.err
+      cat $O/ab_shared.txt
+      B2="$B,\"queue_shared\":0"
+      EXTRA_SCHEDS="s0b8={$B2,\"queue_block\":8192};s0b16={$B2,\"queue_block\":16384};s0b4={$B2,\"queue_block\":4096};s0b8f56={$B2,\"queue_block\":8192,\"fetch_threshold\":56}" \
+      SCHEDS=s0b8,s0b16,s0b4,s0b8f56 ORDERS=fwd REPS=7 ORDER=1 BLOCK=1024 \
+        timeout -k 10 600 python -u tools/strong_diag.py > $O/shard_shared0.txt 2> $O/shard_shared0.err || fail diag $O/shard_shared0.err ;;
     ao_knobs)
       V=""
       for c in '{"autotune":0}' '{"autotune":0,"spec_slack":4}' '{"autotune":0,"tail_lanes":8}' '{"autotune":0,"tail_lanes":4}' \
