@@ -13,6 +13,7 @@
 #   shard_sched  live blocks first, 1024-ray blocks: the shards under slack / waves / tail / lane-group variants
 #   shard_knobs  live blocks first, 1024-ray blocks: shared share / static rounds / refill threshold / tail lanes
 #   shared_frame the shared-queue share on the 1 spp hairball frames and on ordered shards (0 / 2 / 5 %)
+#   balance_final  the saved per-XCD schedule on ordered shards: dist block 512/1024/2048 x cyclic/balanced deal
 #   ao_knobs     Mori / Fairy AO under launch knobs the autotuner does not explore
 #   timeline_shard  per-ray timeline of shard 0, live first vs frame order (variants/tailtl build)
 # Usage: gpurun -- 'bash tools/gpu_experiments.sh order order2'
@@ -114,6 +115,12 @@ print('block $B balance $BAL T1', d['t1_ms'], 'one-stream', d.get('one_stream_ms
       EXTRA_SCHEDS="s0b8={$B2,\"queue_block\":8192};s0b16={$B2,\"queue_block\":16384};s0b4={$B2,\"queue_block\":4096};s0b8f56={$B2,\"queue_block\":8192,\"fetch_threshold\":56}" \
       SCHEDS=s0b8,s0b16,s0b4,s0b8f56 ORDERS=fwd REPS=7 ORDER=1 BLOCK=1024 \
         timeout -k 10 600 python -u tools/strong_diag.py > $O/shard_shared0.txt 2> $O/shard_shared0.err || fail diag $O/shard_shared0.err ;;
+    balance_final)
+      X='"autotune":0,"num_queues":8,"fetch_threshold":56,"waves_per_cu":20,"spec_slack":6,"queue_block":8192,"queue_shared":0'
+      for BL in 512 1024 2048; do for BAL in 0 1; do
+        EXTRA_SCHEDS="c2={$X}" SCHEDS=c2 ORDERS=fwd REPS=9 ORDER=1 BLOCK=$BL BALANCE=$BAL \
+          timeout -k 10 300 python -u tools/strong_diag.py > $O/bal_b${BL}_$BAL.txt 2> $O/bal_b${BL}_$BAL.err || fail diag $O/bal_b${BL}_$BAL.err
+      done; done ;;
     ao_knobs)
       V=""
       for c in '{"autotune":0}' '{"autotune":0,"spec_slack":4}' '{"autotune":0,"tail_lanes":8}' '{"autotune":0,"tail_lanes":4}' \
