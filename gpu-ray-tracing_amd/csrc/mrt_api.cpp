@@ -203,8 +203,6 @@ constexpr int kTunedLaneGroups = 16;
 constexpr int kTunedTailLanes = 16;
 constexpr int kDefaultTailLanes = MRT_DEFAULT_TAIL_LANES;
 
-
-
 mrt_launch_cfg default_cfg() {
     mrt_launch_cfg c;
     c.waves_per_cu = 0;   // auto: sized from the batch (grid_blocks)
@@ -397,7 +395,6 @@ int workspace_for(mrt_tracer* t, void* stream, int totalLanes, int ldsStack, int
         MRT_HIP(hipMalloc(&w->spill, need * sizeof(int)));
         w->spillInts = need;
     }
-
     if (!t->evStart) {
         // the blocking call's timing pair: no system-scope fence around the kernel (it would
         // flush the caches and be timed with it); the stop event releases to device scope,
