@@ -221,7 +221,9 @@ def test_exact_reciprocal_is_correctly_rounded_for_every_float(tracer):
                                  dict(num_queues=8, queue_shared=15, fetch_threshold=48, waves_per_cu=20),
                                  dict(num_queues=8, queue_shared=10, queue_block=4096, fetch_threshold=48, waves_per_cu=4),
                                  dict(num_queues=8, queue_block=64, waves_per_cu=4),
-                                 dict(num_queues=5, queue_shared=5, queue_block=1024, fetch_threshold=40, waves_per_cu=4)],
+                                 dict(num_queues=5, queue_shared=5, queue_block=1024, fetch_threshold=40, waves_per_cu=4),
+                                 dict(num_queues=8, queue_block=8192, fetch_threshold=56, waves_per_cu=20),
+                                 dict(num_queues=8, queue_block=256, fetch_threshold=56, waves_per_cu=4)],
                          ids=lambda c: ",".join(f"{k}={v}" for k, v in c.items()))
 def test_launch_configs_do_not_change_results(tracer, cfg):
     bufs, rays, any_hit, want, st = scene_setup("conference", 256, 192, "diffuse")
