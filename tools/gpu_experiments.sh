@@ -14,6 +14,7 @@
 #   shard_knobs  live blocks first, 1024-ray blocks: shared share / static rounds / refill threshold / tail lanes
 #   shared_frame the shared-queue share on the 1 spp hairball frames and on ordered shards (0 / 2 / 5 %)
 #   balance_final  the saved per-XCD schedule on ordered shards: dist block 512/1024/2048 x cyclic/balanced deal
+#   shard_split  each ordered shard as 1 / 2 / 3 launches alternating over two streams (explicit schedule)
 #   ao_knobs     Mori / Fairy AO under launch knobs the autotuner does not explore
 #   timeline_shard  per-ray timeline of shard 0, live first vs frame order (variants/tailtl build)
 # Usage: gpurun -- 'bash tools/gpu_experiments.sh order order2'
@@ -121,6 +122,12 @@ print('block $B balance $BAL T1', d['t1_ms'], 'one-stream', d.get('one_stream_ms
         EXTRA_SCHEDS="c2={$X}" SCHEDS=c2 ORDERS=fwd REPS=9 ORDER=1 BLOCK=$BL BALANCE=$BAL \
           timeout -k 10 300 python -u tools/strong_diag.py > $O/bal_b${BL}_$BAL.txt 2> $O/bal_b${BL}_$BAL.err || fail diag $O/bal_b${BL}_$BAL.err
       done; done ;;
+    shard_split)
+      X='"autotune":0,"num_queues":8,"fetch_threshold":56,"waves_per_cu":20,"spec_slack":6,"queue_block":8192,"queue_shared":0'
+      for SP in 1 2 3; do
+        EXTRA_SCHEDS="c2={$X}" SCHEDS=c2 ORDERS=fwd REPS=9 ORDER=1 BLOCK=1024 SPLIT=$SP \
+          timeout -k 10 300 python -u tools/strong_diag.py > $O/split_$SP.txt 2> $O/split_$SP.err || fail diag $O/split_$SP.err
+      done ;;
     ao_knobs)
       V=""
       for c in '{"autotune":0}' '{"autotune":0,"spec_slack":4}' '{"autotune":0,"tail_lanes":8}' '{"autotune":0,"tail_lanes":4}' \

@@ -121,6 +121,30 @@ def main():
                 step()
             torch.cuda.synchronize()
             print(f"{name:10s} T1 {ns} stream(s): {(time.perf_counter() - t0) / reps * 1e3:.4f} ms", flush=True)
+        split = int(os.environ.get("SPLIT", "1"))
+        if split > 1:
+            # each shard as `split` launches alternating over the two streams, joined per step
+            for k, rb, live in shards:
+                gos = [tracer.launcher(rb.view(a, b), exact_rcp=True, stream=streams[i % 2])
+                       for i, (a, b) in enumerate(shard_launches(0, rb.size, 1 << 21, split))]
+
+                def sstep():
+                    streams[1].wait_stream(streams[0])
+                    for go in gos:
+                        with torch.cuda.stream(go.stream):
+                            go()
+                    streams[0].wait_stream(streams[1])
+                for _ in range(3):
+                    sstep()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    sstep()
+                torch.cuda.synchronize()
+                print(f"{name:10s} fwd shard {k}: rays {rb.size} live {live} median "
+                      f"{(time.perf_counter() - t0) / reps * 1e3:.4f} ms (split {split})", flush=True)
+            tracer.set_config(**{kk: base[kk] for kk in cfg})
+            continue
         for order in os.environ.get("ORDERS", "fwd,rev").split(","):
             seq = shards if order == "fwd" else shards[::-1]
             for k, rb, live in seq:
