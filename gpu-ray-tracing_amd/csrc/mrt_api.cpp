@@ -125,9 +125,6 @@ struct Workspace {
                                   // (sticky); [kTimedSlot] = the current blocking launch's own count
     int* spill = nullptr;
     size_t spillInts = 0;
-    int* liveCounts = nullptr;    // cfg.live_first: live rays per 1024-ray block, and the blocks' order
-    int* liveOrder = nullptr;
-    size_t liveBlocks = 0;
     // -DMRT_DONE_EVENT: recorded after every launch that uses this scratch, so waiting
     // for it never touches the stream (see workspace_wait)
     hipEvent_t done = nullptr;
@@ -220,7 +217,6 @@ mrt_launch_cfg default_cfg() {
     c.tail_lanes = kDefaultTailLanes;
     c.queue_shared = 0;
     c.queue_block = 0;
-    c.live_first = 0;
     return c;
 }
 
@@ -233,8 +229,7 @@ bool valid_cfg(const mrt_launch_cfg& c) {
            c.static_rounds >= 1 && c.static_rounds <= 64 && (c.autotune == 0 || c.autotune == 1) &&
            c.tail_lanes >= 0 && c.tail_lanes <= 16 &&
            c.queue_shared >= 0 && c.queue_shared <= 100 && c.queue_block >= 0 && c.queue_block <= (1 << 20) &&
-           (c.queue_block & (c.queue_block - 1)) == 0 && (c.queue_block == 0 || c.queue_block >= 64) &&
-           (c.live_first == 0 || c.live_first == 1);
+           (c.queue_block & (c.queue_block - 1)) == 0 && (c.queue_block == 0 || c.queue_block >= 64);
 }
 
 // The frontier tail runs in the exact 4-wide kernels whose leaf refs carry counts.
@@ -512,7 +507,6 @@ mrt_launch_cfg tune_candidate(const mrt_launch_cfg& base, int c, int stage1) {
     x.num_queues = -1;
     x.queue_block = 0;
     x.queue_shared = 0;
-    x.live_first = 0;
     switch (c) {
         case 0: break;                                                      // static rounds, 20 waves/CU
         case 1: x.waves_per_cu = 8; break;                                  // static rounds, fewer waves
@@ -704,23 +698,6 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     a.totalLanes = totalLanes;
     a.stackCap = stackCap;
     a.stackBound = wide ? t->wideStackBound : stackCap - 1;
-    // live-first dispatch: queue modes only (the strided rounds have no dispatch order to
-    // change), and only batches of at least two blocks
-    if (cfg.live_first && a.numQueues > 0 && numRays >= (2 << mrt::kLiveBlockLog2)) {
-        const size_t nBlocks = (size_t)(((int64_t)numRays + (1 << mrt::kLiveBlockLog2) - 1) >> mrt::kLiveBlockLog2);
-        if (nBlocks > ws->liveBlocks) {
-            if (int rc = workspace_wait(ws)) return rc;   // the smaller arrays may still be in use
-            if (ws->liveCounts) MRT_HIP(hipFree(ws->liveCounts));
-            if (ws->liveOrder) MRT_HIP(hipFree(ws->liveOrder));
-            ws->liveCounts = ws->liveOrder = nullptr;
-            ws->liveBlocks = 0;
-            MRT_HIP(hipMalloc(&ws->liveCounts, nBlocks * sizeof(int)));
-            MRT_HIP(hipMalloc(&ws->liveOrder, nBlocks * sizeof(int)));
-            ws->liveBlocks = nBlocks;
-        }
-        a.blockOrder = ws->liveOrder;
-        a.liveOrderLog2 = mrt::kLiveBlockLog2;
-    }
     a.tailLanes = cfg.tail_lanes;
     a.queues = ws->queues;
     a.spill = ws->spill;
@@ -736,8 +713,6 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     if (info) MRT_HIP(hipMemsetAsync(ws->status + mrt::kTimedSlot, 0, sizeof(int), s));
     if (info) MRT_HIP(hipEventRecord(t->evStart, s));
     if (slot) MRT_HIP(hipEventRecord(slot->start, s));
-    if (a.liveOrderLog2 > 0)   // inside the timed region: the ordering is part of the launch's cost
-        MRT_HIP(mrt::launch_live_order(a.rays, numRays, a.liveOrderLog2, ws->liveCounts, ws->liveOrder, s));
     MRT_HIP(mrt::launch_trace(v, a, blocks, s));
 #ifdef MRT_DONE_EVENT
     MRT_HIP(hipEventRecord(ws->done, s));
@@ -873,8 +848,6 @@ int mrt_tracer_destroy(mrt_tracer* t) {
             if (w->queues) (void)hipFree(w->queues);
             if (w->status) (void)hipFree(w->status);
             if (w->spill) (void)hipFree(w->spill);
-            if (w->liveCounts) (void)hipFree(w->liveCounts);
-            if (w->liveOrder) (void)hipFree(w->liveOrder);
             delete w;
         }
         if (t->evStart) (void)hipEventDestroy(t->evStart);

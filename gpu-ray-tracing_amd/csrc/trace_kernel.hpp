@@ -54,8 +54,6 @@ struct TraceArgs {
                                // keeps this much headroom before it expands more than one entry per step
     int tailLanes;            // exact 4-wide speculative kernels: a wave that cannot refill and is down to
                                // this many live lanes finishes them in the frontier tail (0 = off)
-    const int* blockOrder;     // liveOrderLog2 > 0: the caller's 2^L-ray block behind each logical block
-    int liveOrderLog2;         // queue modes with cfg.live_first: logical ray r is block blockOrder[r >> L]'s ray
     unsigned* queues;          // numQueues heads, kQueueStrideWords apart, zeroed per launch
     int* spill;                // (stackCap - S) * totalLanes ints
     int* status;               // [0] = stack overflow count (entries pushed past stackCap)
@@ -96,12 +94,6 @@ int64_t wide_stack_bound(const uint32_t* wide, int64_t numWide, int nodeWords);
 // output) when some child box has no finite quantization (non-finite planes).
 bool build_wide4q(const int32_t* nodes, int64_t numNodes, std::vector<uint32_t>* out, const int32_t* woopX = nullptr,
                   int64_t woopSlots = 0);
-
-// Live-first dispatch order of a batch (cfg.live_first): per 2^log2B-ray block its live
-// rays (tmax >= 0) into counts[nBlocks], then order[] = the full blocks, most live rays
-// first, and the partial last block last. log2B in 8..10; stream-ordered.
-constexpr int kLiveBlockLog2 = 10;
-hipError_t launch_live_order(const float4* rays, int numRays, int log2B, int* counts, int* order, hipStream_t s);
 
 // Launch one persistent trace. grid = number of 256-thread workgroups.
 hipError_t launch_trace(const TraceVariant& v, const TraceArgs& a, int gridBlocks, hipStream_t s);

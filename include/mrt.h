@@ -119,12 +119,6 @@ typedef struct mrt_launch_cfg {
     int32_t queue_block;       /* num_queues > 1: 0 = each queue's share is contiguous; a power of two >= 64 =
                                   the shares are this many rays' blocks dealt cyclically (block i to queue
                                   i mod num_queues), so every XCD samples the whole frame              */
-    int32_t live_first;        /* queue modes (num_queues >= 1): 1 = hand the batch's 1024-ray blocks out
-                                  in order of their live rays (tmax >= 0), most first, instead of the
-                                  caller's order (two small kernels per launch count and order them; rays
-                                  and results stay where the caller put them); 0 = the caller's order
-                                  (default 0, opt-in: hairball diffuse 1920x1080 in pixel order -4 %, an
-                                  already cost-ordered buffer +4 %, the 307k-ray batches +5..+18 %)    */
 } mrt_launch_cfg;
 
 /* Per-launch statistics reported back to the host (optional). */

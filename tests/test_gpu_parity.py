@@ -223,8 +223,7 @@ def test_exact_reciprocal_is_correctly_rounded_for_every_float(tracer):
                                  dict(num_queues=8, queue_block=64, waves_per_cu=4),
                                  dict(num_queues=5, queue_shared=5, queue_block=1024, fetch_threshold=40, waves_per_cu=4),
                                  dict(num_queues=8, queue_block=8192, fetch_threshold=56, waves_per_cu=20),
-                                 dict(num_queues=8, queue_block=256, fetch_threshold=56, waves_per_cu=4),
-                                 dict(num_queues=8, queue_block=8192, fetch_threshold=56, live_first=1)],
+                                 dict(num_queues=8, queue_block=256, fetch_threshold=56, waves_per_cu=4)],
                          ids=lambda c: ",".join(f"{k}={v}" for k, v in c.items()))
 def test_launch_configs_do_not_change_results(tracer, cfg):
     bufs, rays, any_hit, want, st = scene_setup("conference", 256, 192, "diffuse")
@@ -235,34 +234,6 @@ def test_launch_configs_do_not_change_results(tracer, cfg):
         assert np.array_equal(res[:, :2], want[:, :2]) and np.array_equal(gst[:, :3], st[:, :3])
         res2, _ = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=True)
         assert np.array_equal(res2[:, :2], want[:, :2])
-    finally:
-        tracer.set_config(**saved)
-
-
-@pytest.mark.parametrize("cfg", [dict(num_queues=8, queue_block=8192, fetch_threshold=56, live_first=1),
-                                 dict(num_queues=8, queue_block=256, fetch_threshold=56, live_first=1, waves_per_cu=4),
-                                 dict(num_queues=1, fetch_threshold=48, live_first=1, waves_per_cu=4),
-                                 dict(num_queues=3, live_first=1, waves_per_cu=4, static_rounds=2),
-                                 dict(live_first=1)],
-                         ids=lambda c: ",".join(f"{k}={v}" for k, v in c.items()))
-@pytest.mark.parametrize("cut", [0, 333])
-def test_live_first_dispatch_keeps_results(tracer, cfg, cut):
-    """cfg.live_first: the queue modes hand out the batch's 1024-ray blocks most live rays
-    first (a count kernel and a single-workgroup counting sort before the trace). A
-    hairball diffuse batch with dead (tmax = -1) rays, whole and with a partial last
-    block: closest hits equal the oracle in speculative and per-lane order, the per-lane
-    counters too (every ray traced once, at its own index); the strided mode ignores it."""
-    bufs, rays, any_hit, want, st = scene_setup("hairball:800", 256, 192, "diffuse")
-    n = len(rays) - cut
-    r, w, s_ = np.ascontiguousarray(rays[:n]), want[:n], st[:n]
-    assert (r[:, 7] < 0).any() and (r[:, 7] >= 0).any()
-    saved = tracer.config()
-    try:
-        tracer.set_config(autotune=0, **cfg)
-        res, _ = gpu_trace(tracer, bufs, r, any_hit, exact=True, spec=True)
-        assert np.array_equal(res[:, :2], w[:, :2])
-        res2, gst = gpu_trace(tracer, bufs, r, any_hit, exact=True, spec=False, stats=True)
-        assert np.array_equal(res2[:, :2], w[:, :2]) and np.array_equal(gst[:, :3], s_[:, :3])
     finally:
         tracer.set_config(**saved)
 

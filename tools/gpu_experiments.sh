@@ -16,7 +16,6 @@
 #   balance_final  the saved per-XCD schedule on ordered shards: dist block 512/1024/2048 x cyclic/balanced deal
 #   shard_split  each ordered shard as 1 / 2 / 3 launches alternating over two streams (explicit schedule)
 #   order_frame  one frame's batch in frame order vs live blocks first (tools/order_probe.py)
-#   live_first   parity subset, then cfg.live_first on the frames and on the strong-scaling shards
 #   ao_knobs     Mori / Fairy AO under launch knobs the autotuner does not explore
 #   timeline_shard  per-ray timeline of shard 0, live first vs frame order (variants/tailtl build)
 # Usage: gpurun -- 'bash tools/gpu_experiments.sh order order2'
@@ -137,20 +136,6 @@ print('block $B balance $BAL T1', d['t1_ms'], 'one-stream', d.get('one_stream_ms
         timeout -k 10 300 python -u tools/order_probe.py $W '{"autotune":0}' 1024 >> $O/order_frame.txt 2>> $O/order_frame.err || fail probe $O/order_frame.err
       done
       cat $O/order_frame.txt ;;
-    live_first)
-      timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
-        -k "live_first or launch_configs or tail" > $O/pytest_live.log 2>&1 || fail pytest $O/pytest_live.log
-      tail -1 $O/pytest_live.log
-      X='"autotune":0,"num_queues":8,"fetch_threshold":56,"waves_per_cu":20,"spec_slack":6,"queue_block":8192,"queue_shared":0'
-      timeout -k 10 600 python -u tools/ab.py --rounds 7 --launches 30 --workload hairball-diffuse-1920x1080 --workload hairball-diffuse-640x480 \
-        --workload sponza-diffuse-640x480 --workload conference-ao-640x480 \
-        --variant "lib:{$X}" --variant "lib:{$X,\"live_first\":1}" --variant 'lib:{"saved":1}' \
-        > $O/ab_live.txt 2> $O/ab_live.err || fail ab $O/ab_live.err
-      cat $O/ab_live.txt
-      for ORD in 0 1; do
-        EXTRA_SCHEDS="c2={$X};c2l={$X,\"live_first\":1}" SCHEDS=c2,c2l ORDERS=fwd REPS=9 ORDER=$ORD BLOCK=1024 \
-          timeout -k 10 300 python -u tools/strong_diag.py > $O/live_ord$ORD.txt 2> $O/live_ord$ORD.err || fail diag $O/live_ord$ORD.err
-      done ;;
     ao_knobs)
       V=""
       for c in '{"autotune":0}' '{"autotune":0,"spec_slack":4}' '{"autotune":0,"tail_lanes":8}' '{"autotune":0,"tail_lanes":4}' \
