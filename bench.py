@@ -608,13 +608,14 @@ SCHEDULES = {0: "static rounds, 20 waves/CU", 1: "static rounds, 8 waves/CU",
 
 
 def schedule_name(c):
-    """mrt_trace_info.autotune_candidate: 0-7 a schedule, 8/9/10/11 (| stage-1 schedule << 8) that
-    schedule with spec_slack 4/6, 16 lane groups or with the frontier tail toggled (off: the library's default
+    """mrt_trace_info.autotune_candidate: 0-7 a schedule, 8/9/10/11/12 (| stage-1 schedule << 8) that
+    schedule with spec_slack 4/6, the frontier tail toggled, 16 lane groups, or 2 lane groups with spec_slack 6 (off: the library's default
     has it on, include/mrt.h tail_lanes), -1 the fixed rule (autotune off or several streams)."""
     if c < 0:
         return "fixed rule"
     if (c & 0xff) >= 8:
-        return f"{SCHEDULES[c >> 8]}, " + {8: "spec_slack 4", 9: "spec_slack 6", 10: "no frontier tail", 11: "16 lane groups"}[c & 0xff]
+        return f"{SCHEDULES[c >> 8]}, " + {8: "spec_slack 4", 9: "spec_slack 6", 10: "no frontier tail", 11: "16 lane groups",
+                                            12: "2 lane groups, spec_slack 6"}[c & 0xff]
     return SCHEDULES[c]
 
 

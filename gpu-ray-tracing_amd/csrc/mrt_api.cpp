@@ -80,7 +80,7 @@ struct TuneState {
     // with the speculation slack at 4 and 6, without the frontier tail (with it if the
     // tracer's default is off), and with 16 lane groups (candidates kSchedules .. + 3).
     static constexpr int kSchedules = 8;
-    static constexpr int kStage2 = 4;
+    static constexpr int kStage2 = 5;
     static constexpr int kCandidates = kSchedules + kStage2;
     static constexpr int kSamples = 8;   // timed launches per candidate; the median ranks them
     int launches = 0;    // exploring launches so far (the first round of candidates runs untimed:
@@ -499,6 +499,13 @@ mrt_launch_cfg tune_candidate(const mrt_launch_cfg& base, int c, int stage1) {
         // tile of expensive rays (a silhouette), so more of them reach the frontier tail early
         // (bunny primary 640x480 0.086 -> 0.069 ms, sponza diffuse +8 %; conference AO -7 %)
         if (k == 3) x.lane_groups = kTunedLaneGroups;
+        // two lane groups with slack 6: the coherent primary batches keep most of their tile
+        // coherence and still shed their expensive half-tiles early (bunny primary 1024x768
+        // +3 %, profiles/round4_head_knobs.txt)
+        if (k == 4 && base.lane_groups == 1 && base.spec_slack == kDefaultSpecSlack) {
+            x.lane_groups = 2;
+            x.spec_slack = 6;
+        }
         return x;
     }
     mrt_launch_cfg x = base;

@@ -97,8 +97,8 @@ typedef struct mrt_launch_cfg {
                                   of each batch size (per kernel variant, up to 64 sizes) time eight ray-
                                   distribution schedules (static rounds at 20, 16, 12 or 8 waves/CU, per-XCD
                                   block-cyclic queues, the global queue at 20, 16 or 12 waves/CU), then
-                                  the winner with spec_slack 4 and 6, without the frontier tail and with 16
-                                  lane groups (each
+                                  the winner with spec_slack 4 and 6, without the frontier tail, with 16
+                                  lane groups, and with 2 lane groups at spec_slack 6 (each
                                   knob only when left at its default), eight times each without blocking,
                                   after one untimed round of them; the median ranks them and a candidate
                                   replaces the fixed rule (stage 1) or the stage-1 winner (stage 2) only
@@ -163,7 +163,7 @@ typedef struct mrt_tuned_schedule {
     int32_t candidate;
     int32_t version;           /* MRT_TUNE_VERSION when exported; others are refused on import */
 } mrt_tuned_schedule;
-enum { MRT_TUNE_VERSION = 9 };
+enum { MRT_TUNE_VERSION = 10 };
 
 /* ---- handle API -------------------------------------------------------- */
 int  mrt_tracer_create(int device, mrt_tracer** out);

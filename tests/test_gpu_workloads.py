@@ -162,7 +162,7 @@ def test_autotuned_schedule_settles_and_keeps_results(env):
         assert np.array_equal(got[:, :2], want[:, :2]), f"launch {i} (candidate {tracer.last_info['autotune_candidate']})"
         if tracer.last_info["autotune_locked"]:
             break
-    assert seen == set(range(12))
+    assert seen == set(range(13))
     assert tracer.last_info["autotune_locked"] == 1
     # the settled choice round-trips through export/import onto a fresh bind
     saved = tracer.schedules()

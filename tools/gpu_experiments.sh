@@ -16,6 +16,7 @@
 #   balance_final  the saved per-XCD schedule on ordered shards: dist block 512/1024/2048 x cyclic/balanced deal
 #   shard_split  each ordered shard as 1 / 2 / 3 launches alternating over two streams (explicit schedule)
 #   order_frame  one frame's batch in frame order vs live blocks first (tools/order_probe.py)
+#   head_knobs   the headline batch under slack / lane-group / tail / stack variants of its saved schedule
 #   ao_knobs     Mori / Fairy AO under launch knobs the autotuner does not explore
 #   timeline_shard  per-ray timeline of shard 0, live first vs frame order (variants/tailtl build)
 # Usage: gpurun -- 'bash tools/gpu_experiments.sh order order2'
@@ -136,6 +137,18 @@ print('block $B balance $BAL T1', d['t1_ms'], 'one-stream', d.get('one_stream_ms
         timeout -k 10 300 python -u tools/order_probe.py $W '{"autotune":0}' 1024 >> $O/order_frame.txt 2>> $O/order_frame.err || fail probe $O/order_frame.err
       done
       cat $O/order_frame.txt ;;
+    head_knobs)
+      V=""
+      for c in '{"autotune":0,"waves_per_cu":8,"spec_slack":6}' '{"autotune":0,"waves_per_cu":8,"spec_slack":8}' \
+               '{"autotune":0,"waves_per_cu":8,"spec_slack":10}' '{"autotune":0,"waves_per_cu":8,"spec_slack":14}' \
+               '{"autotune":0,"waves_per_cu":8,"spec_slack":20}' '{"autotune":0,"waves_per_cu":8,"spec_slack":6,"lane_groups":2}' \
+               '{"autotune":0,"waves_per_cu":8,"spec_slack":6,"tail_lanes":8}' '{"autotune":0,"waves_per_cu":8,"spec_slack":6,"lds_stack":8}' \
+               '{"autotune":0,"waves_per_cu":12,"spec_slack":8}'; do
+        V="$V --variant lib:$c"
+      done
+      timeout -k 10 600 python -u tools/ab.py --rounds 9 --launches 30 --workload bunny-primary-1024x768 --workload bunny-primary-640x480 $V \
+        > $O/ab_head.txt 2> $O/ab_head.err || fail ab $O/ab_head.err
+      cat $O/ab_head.txt ;;
     ao_knobs)
       V=""
       for c in '{"autotune":0}' '{"autotune":0,"spec_slack":4}' '{"autotune":0,"tail_lanes":8}' '{"autotune":0,"tail_lanes":4}' \

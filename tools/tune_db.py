@@ -24,7 +24,7 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "gpu-ray-tracing_amd"))
 
 MARGIN = 0.03
-N_SCHEDULES, STAGE2 = 8, 4
+N_SCHEDULES, STAGE2 = 8, 5
 
 
 def variant_key(any_hit, exact, lds_stack=16, nodes=1, tail=False):
