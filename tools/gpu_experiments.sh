@@ -17,6 +17,7 @@
 #   shard_split  each ordered shard as 1 / 2 / 3 launches alternating over two streams (explicit schedule)
 #   order_frame  one frame's batch in frame order vs live blocks first (tools/order_probe.py)
 #   head_knobs   the headline batch under slack / lane-group / tail / stack variants of its saved schedule
+#   head_knobs2  the headline's new schedule against its neighbours (lane groups 2/4, slack 4/6/8, waves 8/12/16)
 #   ao_knobs     Mori / Fairy AO under launch knobs the autotuner does not explore
 #   timeline_shard  per-ray timeline of shard 0, live first vs frame order (variants/tailtl build)
 # Usage: gpurun -- 'bash tools/gpu_experiments.sh order order2'
@@ -149,6 +150,17 @@ print('block $B balance $BAL T1', d['t1_ms'], 'one-stream', d.get('one_stream_ms
       timeout -k 10 600 python -u tools/ab.py --rounds 9 --launches 30 --workload bunny-primary-1024x768 --workload bunny-primary-640x480 $V \
         > $O/ab_head.txt 2> $O/ab_head.err || fail ab $O/ab_head.err
       cat $O/ab_head.txt ;;
+    head_knobs2)
+      V=""
+      for c in '{"autotune":0,"waves_per_cu":8,"spec_slack":6,"lane_groups":2}' '{"autotune":0,"waves_per_cu":8,"spec_slack":6,"lane_groups":4}' \
+               '{"autotune":0,"waves_per_cu":8,"spec_slack":4,"lane_groups":2}' '{"autotune":0,"waves_per_cu":8,"spec_slack":8,"lane_groups":2}' \
+               '{"autotune":0,"waves_per_cu":12,"spec_slack":6,"lane_groups":2}' '{"autotune":0,"waves_per_cu":8,"spec_slack":6,"lane_groups":2,"tail_lanes":12}' \
+               '{"autotune":0,"waves_per_cu":8,"spec_slack":6,"lane_groups":2,"static_rounds":1}' '{"autotune":0,"waves_per_cu":16,"spec_slack":6,"lane_groups":4}'; do
+        V="$V --variant lib:$c"
+      done
+      timeout -k 10 600 python -u tools/ab.py --rounds 9 --launches 30 --workload bunny-primary-1024x768 --workload fairy-ao-640x480 --workload mori-ao-640x480 $V \
+        > $O/ab_head2.txt 2> $O/ab_head2.err || fail ab $O/ab_head2.err
+      cat $O/ab_head2.txt ;;
     ao_knobs)
       V=""
       for c in '{"autotune":0}' '{"autotune":0,"spec_slack":4}' '{"autotune":0,"tail_lanes":8}' '{"autotune":0,"tail_lanes":4}' \
