@@ -63,6 +63,8 @@ def main():
               f"{tail.sum()} of {len(end)} rays finished in the tail", flush=True)
         for q in (50, 90, 99, 99.9, 100):
             print(f"   {q:5}% of rays done by {np.percentile(end, q):7.1f} us")
+        print("   ray starts (with a -DMRT_TAIL_TIMELINE=3 build: a lane's first ray = its wave's start): "
+              + " ".join(f"p{q}:{np.percentile(start, q):.1f}" for q in (1, 10, 50, 90, 99, 100)) + " us")
         # the last fetch: the queue (or the strided rounds) ran dry here; what was in flight then
         dry = start.max()
         fl = (start <= dry) & (end > dry)
