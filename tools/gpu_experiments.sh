@@ -18,6 +18,7 @@
 #   order_frame  one frame's batch in frame order vs live blocks first (tools/order_probe.py)
 #   head_knobs   the headline batch under slack / lane-group / tail / stack variants of its saved schedule
 #   head_knobs2  the headline's new schedule against its neighbours (lane groups 2/4, slack 4/6/8, waves 8/12/16)
+#   small_xcd    per-XCD queues with smaller blocks on the 307 k-ray batches (vs their saved schedules)
 #   ao_knobs     Mori / Fairy AO under launch knobs the autotuner does not explore
 #   timeline_shard  per-ray timeline of shard 0, live first vs frame order (variants/tailtl build)
 # Usage: gpurun -- 'bash tools/gpu_experiments.sh order order2'
@@ -161,6 +162,14 @@ print('block $B balance $BAL T1', d['t1_ms'], 'one-stream', d.get('one_stream_ms
       timeout -k 10 600 python -u tools/ab.py --rounds 9 --launches 30 --workload bunny-primary-1024x768 --workload fairy-ao-640x480 --workload mori-ao-640x480 $V \
         > $O/ab_head2.txt 2> $O/ab_head2.err || fail ab $O/ab_head2.err
       cat $O/ab_head2.txt ;;
+    small_xcd)
+      V='--variant lib:{"saved":1}'
+      for B in 1024 2048 4096; do for W in 12 20; do
+        V="$V --variant lib:{\"autotune\":0,\"num_queues\":8,\"fetch_threshold\":56,\"waves_per_cu\":$W,\"spec_slack\":6,\"queue_block\":$B}"
+      done; done
+      timeout -k 10 600 python -u tools/ab.py --rounds 9 --launches 30 --workload hairball-diffuse-640x480 --workload hairball-primary-640x480 \
+        --workload sponza-diffuse-640x480 $V > $O/ab_small_xcd.txt 2> $O/ab_small_xcd.err || fail ab $O/ab_small_xcd.err
+      cat $O/ab_small_xcd.txt ;;
     ao_knobs)
       V=""
       for c in '{"autotune":0}' '{"autotune":0,"spec_slack":4}' '{"autotune":0,"tail_lanes":8}' '{"autotune":0,"tail_lanes":4}' \
