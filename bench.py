@@ -821,7 +821,7 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
             shard_ms = []
             for r_ in range(k):
                 sb = shard_buffer(k, r_)
-                w, _, _ = time_steps(shard_steps(sb), steps, 1, 1)
+                w, _, _ = time_steps(shard_steps(sb), steps, 3, 1)
                 shard_ms.append(w / steps * 1e3)
                 del sb
             projected[str(k)] = {"tn_ms": round(max(shard_ms), 4), "eta": round(t1 / (k * max(shard_ms)), 4),
@@ -967,7 +967,7 @@ def main():
                     help="also measure the AO/diffuse/hairball configs (default on at N=1)")
     ap.add_argument("--no-extra", dest="extra", action="store_false")
     ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling measurement")
-    ap.add_argument("--strong-steps", type=int, default=10)
+    ap.add_argument("--strong-steps", type=int, default=50)
     ap.add_argument("--strong-block", type=int, default=STRONG["block"],
                     help="block-cyclic shard block (rays); 0 = contiguous shards")
     ap.add_argument("--strong-balance", type=int, default=int(STRONG["balance"]), choices=[0, 1],
