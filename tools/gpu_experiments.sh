@@ -19,6 +19,7 @@
 #   head_knobs   the headline batch under slack / lane-group / tail / stack variants of its saved schedule
 #   head_knobs2  the headline's new schedule against its neighbours (lane groups 2/4, slack 4/6/8, waves 8/12/16)
 #   small_xcd    per-XCD queues with smaller blocks on the 307 k-ray batches (vs their saved schedules)
+#   deal_rot     ordered shards: block-cyclic deal vs the deal rotated by one rank per round
 #   ao_knobs     Mori / Fairy AO under launch knobs the autotuner does not explore
 #   timeline_shard  per-ray timeline of shard 0, live first vs frame order (variants/tailtl build)
 # Usage: gpurun -- 'bash tools/gpu_experiments.sh order order2'
@@ -170,6 +171,12 @@ print('block $B balance $BAL T1', d['t1_ms'], 'one-stream', d.get('one_stream_ms
       timeout -k 10 600 python -u tools/ab.py --rounds 9 --launches 30 --workload hairball-diffuse-640x480 --workload hairball-primary-640x480 \
         --workload sponza-diffuse-640x480 $V > $O/ab_small_xcd.txt 2> $O/ab_small_xcd.err || fail ab $O/ab_small_xcd.err
       cat $O/ab_small_xcd.txt ;;
+    deal_rot)
+      X='"autotune":0,"num_queues":8,"fetch_threshold":56,"waves_per_cu":20,"spec_slack":6,"queue_block":8192,"queue_shared":0'
+      for D in cyc rot; do
+        EXTRA_SCHEDS="c2={$X}" SCHEDS=c2 ORDERS=fwd REPS=15 ORDER=1 BLOCK=1024 DEAL=$D \
+          timeout -k 10 300 python -u tools/strong_diag.py > $O/deal_$D.txt 2> $O/deal_$D.err || fail diag $O/deal_$D.err
+      done ;;
     ao_knobs)
       V=""
       for c in '{"autotune":0}' '{"autotune":0,"spec_slack":4}' '{"autotune":0,"tail_lanes":8}' '{"autotune":0,"tail_lanes":4}' \

@@ -44,6 +44,10 @@ def main():
     n = big.shape[0]
     weights = block_weights(big, block)
     owners = balance_blocks(weights, world) if balance else None
+    if os.environ.get("DEAL") == "rot":   # block-cyclic with the deal rotated by one rank per round
+        import numpy as np
+        nb = len(weights)
+        owners = ((np.arange(nb) + np.arange(nb) // world) % world).astype(np.int32)
     prio = weights if int(os.environ.get("ORDER", "0")) else None   # costly (live) blocks first in each shard
     shards = []
     for k in range(world):
