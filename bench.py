@@ -752,9 +752,10 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
         return RayBuffer(local_rays(big.rays, shard_spans(n, k, rk, cfg["block"], owners_for(k), prio)),
                          need_closest_hit=True)
 
-    if prio is not None:   # T_1's buffer in the same block order (its results are gathered back the same way)
-        big_local = shard_buffer(1, 0)
-    local = (big_local if prio is not None else big) if world == 1 else shard_buffer(world, rank)
+    if world == 1:   # T_1's buffer: the whole frame, in the same block order as the shards when they are ordered
+        local = shard_buffer(1, 0) if prio is not None else big
+    else:
+        local = shard_buffer(world, rank)
     torch.cuda.synchronize()
     # The shard's <= 2^21-ray launches are independent batches: they alternate
     # between two streams (each stream has its own trace scratch), so one
