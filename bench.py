@@ -12,7 +12,10 @@ stand-ins with the published triangle counts (the OBJ assets are absent).
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME] [--extra/--no-extra]
                   [--scaling weak|strong]
 
-Multi-GPU (torch.distributed.run, one rank per GPU, RCCL): rank 0 builds the
+Multi-GPU (one rank per GPU, RCCL): under torch.distributed.run (WORLD_SIZE set)
+every process is one rank; `python bench.py --gpus N` without a launcher starts
+its N ranks itself as child processes before any GPU call (launch_ranks), relays
+rank 0's line and exits non-zero if any rank failed. Rank 0 builds the
 SBVH and broadcasts the Compact2 buffers, which stay in HBM (the BVH is
 replicated). Two scalings are measured in every run:
 
@@ -59,6 +62,8 @@ LINE_BYTES = 128         # gfx950 L1 and L2 line: one TCP_TCC_READ_REQ / TCC_EA0
 MALL_BYTES = 256 << 20   # Infinity Cache: a BVH above this streams from HBM
 PROFILE_TAGS = ("round4",)   # committed rocprofv3 summaries the line may cite, newest first
                                       # (profiles/<tag>_<workload>_*): only one of the timed schedule is cited
+PROFILE_RATIO = (0.9, 1.1)   # a cited profile's mean kernel time / this run's event time must lie in here
+LATENCY_BOUND = 0.25         # every memory level served below this fraction of its ceiling: bound = "latency"
 LINE_MAX_BYTES = 10_000  # the driver parses one stdout line; round 3's 21.7 kB line was not parsed
 STORE = None             # mrt.schedules.ScheduleStore the tracer's schedules are locked from (main())
 LEARNED = None           # ScheduleStore collecting the schedules this run settled (--save-schedules)
@@ -145,6 +150,23 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+LINE_OUT = None   # the stream the one JSON line goes to (reserve_line_stdout)
+
+
+def reserve_line_stdout():
+    """Keep the process's stdout for the one JSON line: the original fd 1 is kept for
+    it and fd 1 itself becomes stderr, so whatever libraries print there (gloo's
+    "[Gloo] Rank r is connected to ..." lines, runtime banners) cannot end up next to
+    the line the driver parses."""
+    global LINE_OUT
+    if LINE_OUT is None:
+        sys.stdout.flush()
+        keep = os.dup(1)
+        os.dup2(2, 1)
+        LINE_OUT = os.fdopen(keep, "w")
+    return LINE_OUT
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -167,6 +189,72 @@ def host_threads():
 DIST_BACKEND = "nccl"
 
 
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv, script=None, poll_s=0.2, grace_s=30.0):
+    """`--gpus N` (N > 1) without a launcher (no WORLD_SIZE in the environment): start
+    N ranks of `script` (this file) as child processes with the torch.distributed.run
+    environment — RANK = LOCAL_RANK = r, WORLD_SIZE = N, MASTER_ADDR 127.0.0.1 and a
+    free port — one per GPU. The parent never touches the GPU (it is called before
+    anything imports the tracer) and never execs: it waits for its children, which
+    inherit its stdout, so rank 0's line is the parent's line. When a rank fails the
+    others are terminated (SIGTERM, then SIGKILL after grace_s: a rank blocked in a
+    collective on a dead peer would wait forever) and its exit code is returned;
+    0 when every rank succeeded. SIGTERM/SIGINT to the parent are passed on."""
+    import signal
+    import subprocess
+    script = os.path.abspath(script or __file__)
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env))
+
+    def stop_all(sig=signal.SIGTERM):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    p.send_signal(sig)
+                except OSError:
+                    pass
+
+    def on_signal(signum, _frame):
+        stop_all(signum)
+        raise SystemExit(128 + signum)
+
+    old = {s: signal.signal(s, on_signal) for s in (signal.SIGTERM, signal.SIGINT)}
+    rc = 0
+    try:
+        while any(p.poll() is None for p in procs):
+            bad = [p for p in procs if p.poll() not in (None, 0)]
+            if bad:
+                rc = bad[0].returncode
+                log(f"[launch] rank {procs.index(bad[0])} exited with {rc}: stopping the other ranks")
+                stop_all()
+                t0 = time.time()
+                while any(p.poll() is None for p in procs) and time.time() - t0 < grace_s:
+                    time.sleep(poll_s)
+                stop_all(signal.SIGKILL)
+                break
+            time.sleep(poll_s)
+        for p in procs:
+            p.wait()
+        if rc == 0:
+            rc = next((p.returncode for p in procs if p.returncode != 0), 0)
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+    return rc if rc > 0 else (1 if rc else 0)
+
+
 def dist_setup(n_gpus, backend="nccl"):
     """One process per GPU. backend "nccl" is RCCL; "gloo" (CPU collectives) is
     only for rehearsing the N>1 flow with several ranks on one GPU."""
@@ -176,7 +264,8 @@ def dist_setup(n_gpus, backend="nccl"):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != n_gpus:
-        raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+        raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={world} (a launcher started this process for another "
+                         f"world size)")
     device = local if backend == "nccl" else local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
     if world > 1:
@@ -361,6 +450,31 @@ def algorithmic_bytes(tracer, batches):
     return total, nodes, tris, leaves
 
 
+def kernel_bytes(tracer, batches):
+    """The bytes the PRODUCTION traversal reads per launch, next to
+    SURVEY §8(d)'s binary-order figure: the speculative kernel's STATS variant counts
+    its own 4-wide node visits, triangle tests and leaf ends (bit-identical closest
+    hits; the STATS launch runs the fixed-rule schedule, so the counts of other
+    schedules differ by the frontier tail's few extra visits). Per ray:
+    32 (ray) + 8 (result) + 128 N_wide + 48 N_tri + 4 [hit] — the wide leaf refs carry
+    their triangle counts, so no terminator slot is read. Returns (bytes, nodes, tris)."""
+    import torch
+    total, nodes, tris = 0, 0, 0
+    for rb, _ in batches:
+        saved = rb.results.clone()
+        tracer.trace_batch(rb, exact_rcp=True, speculative=True, stats=True)
+        li = tracer.last_info   # node_bytes: 128 for the 4-wide lines, 64 for Compact2 (wide nodes off)
+        s = rb.stats.to(torch.int64)
+        hits = (rb.results[:, 0] != -1).to(torch.int64).sum().item()
+        n, t, lv = s[:, 0].sum().item(), s[:, 1].sum().item(), s[:, 2].sum().item()
+        nodes, tris = nodes + n, tris + t
+        term = 16 * lv if li["wide"] != 4 else 0   # binary leaves end on a -0.0 terminator slot
+        total += 40 * rb.size + li["node_bytes"] * n + 48 * t + term + 4 * hits
+        rb.results.copy_(saved)
+        rb.stats = None
+    return total, nodes, tris
+
+
 def joined(launches):
     """The launches of one step, as one callable. When they span several streams the
     step is a frame: its other streams wait for everything enqueued on the first
@@ -530,7 +644,7 @@ def cpu_baseline(batches, bufs, counted, threads, label, fast_results=None):
     return out
 
 
-def roofline(name, alg_bytes_per_launch, kernel_ms, bvh_bytes, schedule, rcp="exact"):
+def roofline(name, alg_bytes_per_launch, kernel_ms, bvh_bytes, schedule, rcp="exact", kernel_bytes_per_launch=None):
     """Roofline of the dominant kernel, as the bench contract defines it: achieved =
     the ALGORITHMIC bytes of SURVEY.md §8(d) per launch (every byte the rays read, from
     the per-ray node/triangle/leaf counts) / this run's HIP-event kernel time, against
@@ -542,7 +656,14 @@ def roofline(name, alg_bytes_per_launch, kernel_ms, bvh_bytes, schedule, rcp="ex
     not clamped: SURVEY §8d). `served` prices what each level actually moved against its
     own ceiling (L1->L2 requests / 34.5 TB/s; fabric / 8.6 TB/s, the Infinity Cache's
     random-row rate) and names the larger as `binding_level`. The cited profile must
-    have run the timed schedule (autotune candidate and its name, grid, queues) or none is cited."""
+    have run the timed schedule (autotune candidate and its name, grid, queues) or none is cited,
+    and its mean kernel time must lie within PROFILE_RATIO of this run's.
+
+    kernel_bytes_per_launch (kernel_bytes(): what the production 4-wide traversal reads)
+    gives `kernel_achieved` / `kernel_frac` beside the binary-order §8(d) figure. `bound` is
+    read from the served fractions, not assumed: "latency" when every level serves under
+    LATENCY_BOUND of its ceiling (dependent fetches of a few lanes per wave, not bandwidth),
+    else "hbm" (the fabric) or "l2" as the binding level; "hbm" when no profile is cited."""
     t = kernel_ms * 1e-3
     alg = alg_bytes_per_launch / t / 1e9
     out = {"bound": "hbm", "achieved": round(alg, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -550,6 +671,10 @@ def roofline(name, alg_bytes_per_launch, kernel_ms, bvh_bytes, schedule, rcp="ex
            "basis": "SURVEY 8(d) algorithmic bytes per launch / HIP-event kernel time; traffic = PMC fabric bytes",
            "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": int(alg_bytes_per_launch),
            "bvh_bytes": int(bvh_bytes), "bvh_exceeds_mall": bvh_bytes > MALL_BYTES}
+    if kernel_bytes_per_launch:
+        kb = kernel_bytes_per_launch / t / 1e9
+        out.update({"kernel_bytes_per_launch": int(kernel_bytes_per_launch), "kernel_achieved": round(kb, 1),
+                    "kernel_frac": round(kb / HBM_PEAK_GBS, 4)})
     if alg > HBM_PEAK_GBS:
         out["note"] = "algorithmic rate above the HBM peak: the BVH is cache-resident (L1/L2 hits)"
     # the schedule's name too: it spells out what the candidate number means in this build (queue blocks, ...)
@@ -560,6 +685,13 @@ def roofline(name, alg_bytes_per_launch, kernel_ms, bvh_bytes, schedule, rcp="ex
         out["profile"] = {"note": f"no committed PMC profile of the timed schedule {want}",
                           "seen": [p["path"] for p in profs]}
         return out
+    ratio = prof["avg_ns"] / 1e6 / kernel_ms
+    if not PROFILE_RATIO[0] <= ratio <= PROFILE_RATIO[1]:
+        # same schedule, but the profiled launch ran at another speed (e.g. the gloo rehearsal's
+        # ranks sharing one GPU): its bytes per launch would be priced against the wrong time
+        out["profile"] = {"note": f"{prof['path']} not cited: its mean kernel time is {ratio:.3f}x this run's "
+                                  f"(outside {PROFILE_RATIO})", "kernel_ms_ratio": round(ratio, 4)}
+        return out
     lv = prof["levels"]
     levels = {"l2": (lv["l2_request_bytes"], L2_PEAK_GBS), "fabric": (lv["fabric_bytes"], MALL_PEAK_GBS)}
     fr = {k: b / t / 1e9 / peak for k, (b, peak) in levels.items()}
@@ -569,6 +701,8 @@ def roofline(name, alg_bytes_per_launch, kernel_ms, bvh_bytes, schedule, rcp="ex
                 "served": {k: {"bytes_per_launch": int(levels[k][0]), "GBps": round(levels[k][0] / t / 1e9, 1),
                                "peak_GBps": levels[k][1], "frac": round(fr[k], 4)} for k in levels},
                 "binding_level": max(fr, key=fr.get),
+                "bound": ("latency" if max(fr.values()) < LATENCY_BOUND
+                          else ("hbm" if max(fr, key=fr.get) == "fabric" else "l2")),
                 "l1_hit_fraction_of_algorithmic": round(max(0.0, 1.0 - lv["l2_request_bytes"] / alg_bytes_per_launch), 4),
                 "l2_hit_rate": prof.get("l2_hit_rate"),
                 "profile": {"path": prof["path"], "kernel_ms": round(prof["avg_ns"] / 1e6, 4),
@@ -609,8 +743,10 @@ SCHEDULES = {0: "static rounds, 20 waves/CU", 1: "static rounds, 8 waves/CU",
 
 def schedule_name(c):
     """mrt_trace_info.autotune_candidate: 0-7 a schedule, 8/9/10/11/12 (| stage-1 schedule << 8) that
-    schedule with spec_slack 4/6, the frontier tail toggled, 16 lane groups, or 2 lane groups with spec_slack 6 (off: the library's default
-    has it on, include/mrt.h tail_lanes), -1 the fixed rule (autotune off or several streams)."""
+    schedule with spec_slack 4/6, the frontier tail toggled, 16 lane groups, or 2 lane groups with spec_slack 6
+    (the tail: off, since the library's default has it on, include/mrt.h tail_lanes); -1 the fixed rule
+    (autotune off, distribution knobs set by the caller, or a batch size launched on several streams before a
+    schedule settled for it — a settled, saved or inherited schedule runs on every stream, mrt_api.cpp)."""
     if c < 0:
         return "fixed rule"
     if (c & 0xff) >= 8:
@@ -633,6 +769,7 @@ def run_workload(name, tracer, scenes, world, rank, steps, warmup, exact, want_c
     e = scenes.get(scene_name)
     batches = Batches(name, e["scene"], e["gbvh"], tracer, rank)
     alg_bytes, n_nodes, n_tris, n_leaves = algorithmic_bytes(tracer, batches.batches)
+    k_bytes, k_nodes, k_tris = kernel_bytes(tracer, batches.batches)
     launches = [tracer.launcher(rb, exact_rcp=exact) for rb, _ in batches.batches]
     wall, launch_ms, warmed = time_steps(launches, steps, warmup, world)
     wall = reduce_over_ranks(wall, world)
@@ -640,6 +777,7 @@ def run_workload(name, tracer, scenes, world, rank, steps, warmup, exact, want_c
     counted = int(reduce_over_ranks(batches.rays_counted, world, "sum"))
     traced = int(reduce_over_ranks(batches.rays_traced, world, "sum"))
     alg_bytes = reduce_over_ranks(alg_bytes, world, "sum") / world   # per-GPU bytes (mean over ranks)
+    k_bytes = reduce_over_ranks(k_bytes, world, "sum") / world
     value = counted * steps / wall / 1e6
     gather = gather_to_root(batches, world) if world > 1 else None
     # the schedule the launches ran on: saved for this BVH (locked at bind), or settled
@@ -664,7 +802,7 @@ def run_workload(name, tracer, scenes, world, rank, steps, warmup, exact, want_c
         fast_block = {"value": round(batches.rays_counted * fsteps / fwall / 1e6, 2), "steps": fsteps,
                       "kernel_ms_per_launch": round(fms, 4), "schedule": fsched,
                       "roofline": roofline(name, alg_bytes / len(batches.batches), fms, g.total_bytes, fsched,
-                                           rcp="fast")}
+                                           rcp="fast", kernel_bytes_per_launch=k_bytes / len(batches.batches))}
     explored = exploration_cost(tracer, g, batches.batches[0][0], exact) if explore else None
     out = {
         "workload": name,
@@ -687,10 +825,14 @@ def run_workload(name, tracer, scenes, world, rank, steps, warmup, exact, want_c
                    if e["stats"] and not e["cached"] else {})},
         "per_ray": {"nodes": round(n_nodes / batches.rays_traced, 2), "tris": round(n_tris / batches.rays_traced, 2),
                     "leaves": round(n_leaves / batches.rays_traced, 2),
-                    "bytes": round(alg_bytes / batches.rays_traced, 1)},
+                    "bytes": round(alg_bytes / batches.rays_traced, 1),
+                    "wide_nodes": round(k_nodes / batches.rays_traced, 2),
+                    "wide_tris": round(k_tris / batches.rays_traced, 2),
+                    "kernel_bytes": round(k_bytes / batches.rays_traced, 1)},
         "schedule": schedule,
         "autotune_exploration": explored,
-        "roofline": roofline(name, alg_bytes / len(batches.batches), launch_ms, g.total_bytes, schedule),
+        "roofline": roofline(name, alg_bytes / len(batches.batches), launch_ms, g.total_bytes, schedule,
+                             kernel_bytes_per_launch=k_bytes / len(batches.batches)),
         "reference_mrays": REFERENCE_MRAYS.get(name),
         "rcp_fast": fast_block,
     }
@@ -729,13 +871,13 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
     big = RayBuffer(torch.cat([b.rays for b in parts]), need_closest_hit=True)
     del parts, r
 
-    # Blocks dealt by live-ray count (balance_blocks) or cyclically: every rank
-    # computes the same deal from the buffer's tmax column (one reduction).
     # Blocks dealt by live-ray count (balance_blocks) or cyclically, and within a shard
     # in frame order or costly (live) blocks first (order): every rank computes the same
-    # deal from the buffer's tmax column (one reduction).
-    weights = (block_weights(big.rays, cfg["block"]) if (cfg["balance"] or cfg["order"]) and cfg["block"] > 0
-               else None)
+    # deal from the buffer's tmax column (one reduction, brought to the host once so
+    # that no later shard_spans call syncs the device — the timed gather calls it
+    # world + 1 times).
+    weights = (block_weights(big.rays, cfg["block"]).cpu().numpy()
+               if (cfg["balance"] or cfg["order"]) and cfg["block"] > 0 else None)
     prio = weights if cfg["order"] else None
     deals = {}
 
@@ -752,11 +894,19 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
         return RayBuffer(local_rays(big.rays, shard_spans(n, k, rk, cfg["block"], owners_for(k), prio)),
                          need_closest_hit=True)
 
+    # Building the shard's buffer (one index_select of its blocks) stays outside the
+    # timed steps — a rank generating its own rays would produce them in shard order —
+    # but it is timed here (max over ranks), so the line can say what a Renderer that
+    # shards an existing buffer pays on top: value_with_gather_and_shard.
+    torch.cuda.synchronize()
+    barrier(world)
+    ts = time.perf_counter()
     if world == 1:   # T_1's buffer: the whole frame, in the same block order as the shards when they are ordered
         local = shard_buffer(1, 0) if prio is not None else big
     else:
         local = shard_buffer(world, rank)
     torch.cuda.synchronize()
+    shard_build_ms = reduce_over_ranks(1e3 * (time.perf_counter() - ts), world)
     # The shard's <= 2^21-ray launches are independent batches: they alternate
     # between two streams (each stream has its own trace scratch), so one
     # launch's tail overlaps the next one's start.
@@ -768,6 +918,14 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
 
     launches = shard_steps(local)
     wall, launch_ms, _ = time_steps(launches, steps, warmup, world)
+    # The schedule each distinct launch size of the shard ran (a settled or
+    # inherited schedule also runs on the second stream, so the label is read back from
+    # the library, not assumed): one more blocking launch per size, after the timed steps.
+    spans_l = shard_launches(0, local.size, cfg["max_batch"], cfg["min_launches"])
+    scheds = {}
+    for a_, b_ in spans_l:
+        if b_ - a_ not in scheds:
+            scheds[b_ - a_] = schedule_of(tracer, local.view(a_, b_), exact)
     one_stream_ms = None
     if world == 1 and len(streams) > 1:
         # the same launches on one stream: the autotuner's (or saved) schedule applies
@@ -775,10 +933,12 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
         one_stream_ms = w1s / steps * 1e3
     shard_roofline = None
     if with_roofline:   # the line's roofline at N > 1: this rank's launches (SURVEY §8(d) bytes, per launch)
-        views = [(local.view(a, b), 0) for a, b in shard_launches(0, local.size, cfg["max_batch"], cfg["min_launches"])]
+        views = [(local.view(a, b), 0) for a, b in spans_l]
         alg, _, _, _ = algorithmic_bytes(tracer, views)
-        sched = schedule_of(tracer, views[0][0], exact)
-        shard_roofline = roofline("hairball-diffuse-1920x1080", alg / len(views), launch_ms, e["gbvh"].total_bytes, sched)
+        kb, _, _ = kernel_bytes(tracer, views)
+        sched = scheds[spans_l[0][1] - spans_l[0][0]]
+        shard_roofline = roofline(f"{cfg['scene']}-diffuse-{cfg['w']}x{cfg['h']}", alg / len(views), launch_ms,
+                                  e["gbvh"].total_bytes, sched, kernel_bytes_per_launch=kb / len(views))
         shard_roofline["note"] = (f"rank {rank}'s {len(views)} launches of <= {cfg['max_batch']} rays on "
                                   f"{len(streams)} streams; kernel_ms = one launch alone")
     per_rank = gather_floats(wall / steps * 1e3, world)
@@ -835,6 +995,10 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
         "eta": round(t1 / (world * tn), 4), "gather_ms": round(gather_ms, 3),
         "eta_with_gather": round(t1 / (world * (tn + gather_ms)), 4),
         "value": round(counted / (tn * 1e-3) / 1e6, 2), "value_with_gather": round(counted / ((tn + gather_ms) * 1e-3) / 1e6, 2),
+        "shard_build_ms": round(shard_build_ms, 3),
+        "value_with_gather_and_shard": round(counted / ((tn + gather_ms + shard_build_ms) * 1e-3) / 1e6, 2),
+        "schedule": {str(k): v for k, v in scheds.items()},
+        "schedule_name": "; ".join(sorted({v["name"] for v in scheds.values()})),
         "gathered_equals_single_gpu": equal, "streams": len(streams), "min_launches": cfg["min_launches"],
         "shards": (((f"{cfg['block']}-ray blocks dealt by live-ray count" if cfg["balance"]
                      else f"block-cyclic, {cfg['block']}-ray blocks")
@@ -850,6 +1014,7 @@ def compact_roofline(rf):
     if rf is None:
         return None
     keep = {k: rf.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel_ms",
+                                   "kernel_achieved", "kernel_frac", "kernel_bytes_per_launch",
                                    "hbm_measured_GBps", "hbm_measured_frac", "binding_level", "l2_hit_rate",
                                    "l1_hit_fraction_of_algorithmic", "alg_bytes_per_launch", "note")
             if rf.get(k) is not None}
@@ -878,7 +1043,8 @@ def compact_workload(r):
     fast = r.get("rcp_fast")
     out = {"workload": r["workload"], "value": r["value"], "reference_mrays": r.get("reference_mrays"),
            "kernel_ms": r["kernel_ms_per_launch"], "schedule": (r.get("schedule") or {}).get("name"),
-           "roofline": {k: rf.get(k) for k in ("frac", "hbm_measured_frac", "binding_level", "traffic")},
+           "roofline": {k: rf.get(k) for k in ("bound", "frac", "kernel_frac", "hbm_measured_frac", "binding_level",
+                                               "traffic")},
            "cpu_baseline": cb and cb["value"], "parity": compact_parity(cb, fast)}
     if fast:
         out["rcp_fast_value"] = fast["value"]
@@ -890,7 +1056,8 @@ def compact_strong(st):
         return None
     keep = {k: st[k] for k in ("workload", "rays_traced", "rays_counted", "n_gpus", "shards", "streams", "t1_ms",
                                "tn_ms", "eta", "gather_ms", "eta_with_gather", "value", "value_with_gather",
-                               "gathered_equals_single_gpu", "collective")}
+                               "shard_build_ms", "value_with_gather_and_shard", "schedule_name",
+                               "gathered_equals_single_gpu", "collective") if k in st}
     keep["per_rank_ms_max_min"] = [max(st["per_rank_ms"]), min(st["per_rank_ms"])]
     keep["value_n1_same_run"] = round(st["rays_counted"] / (st["t1_ms"] * 1e-3) / 1e6, 2)
     if st.get("projected_from_one_gpu"):
@@ -911,6 +1078,7 @@ def make_line(args, world, head, extras, strong, tracer_cfg):
         value, ms_step = strong["value"], strong["tn_ms"]
         config = {"workload": strong["workload"], "scene": STRONG["scene"], "width": STRONG["w"],
                   "height": STRONG["h"], "samples_per_pixel": STRONG["spp"], "rays_total": strong["rays_traced"],
+                  "rays_counted": strong["rays_counted"],
                   "ray_type": "diffuse", "rcp": args.rcp,
                   "parallelism": ((f"one RayBuffer in {world} shards of {STRONG['block']}-ray blocks "
                                    + ("dealt by live-ray count" if STRONG["balance"] else "dealt round-robin (block-cyclic)")
@@ -926,7 +1094,10 @@ def make_line(args, world, head, extras, strong, tracer_cfg):
                   "parallelism": (f"rays sharded by pixel sample x{world}, BVH replicated "
                                   f"(weak: one {spec[1]}x{spec[2]} sample per GPU, no collective in the step)")}
         steps = args.steps
-    config["schedule"] = (head.get("schedule") or {}).get("name") if args.scaling == "weak" else "fixed rule"
+    # the schedule the timed launches ran, as the library reports it (mrt_trace_info.autotune_candidate):
+    # the headline batch's at N = 1, the shards' launches at N > 1
+    config["schedule"] = ((head.get("schedule") or {}).get("name") if args.scaling == "weak"
+                          else strong.get("schedule_name"))
     line = {
         "metric": METRIC, "value": value, "unit": "Mrays/s", "n_gpus": world, "steps": steps,
         "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": args.scaling,
@@ -979,6 +1150,10 @@ def main():
                     help="caller streams the strong-scaling launches alternate over")
     ap.add_argument("--strong-min-launches", type=int, default=STRONG["min_launches"],
                     help="cut every strong-scaling shard into at least this many launches")
+    ap.add_argument("--strong-scene", default=STRONG["scene"],
+                    help="scene of the strong-scaling RayBuffer (default: BASELINE configs[4]'s hairball)")
+    ap.add_argument("--strong-size", default=f"{STRONG['w']}x{STRONG['h']}x{STRONG['spp']}",
+                    help="WxHxSPP of the strong-scaling diffuse frame (default 1920x1080x8: 16.6 M rays)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--waves-per-cu", type=int, default=0)
     ap.add_argument("--fetch-threshold", type=int, default=-1)
@@ -998,6 +1173,10 @@ def main():
     ap.add_argument("--no-explore", action="store_true", help="skip measuring the autotuner's exploration cost")
     ap.add_argument("--no-fast", action="store_true", help="skip the fast-reciprocal (v_rcp_f32) measurement")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: this process starts the ranks and only waits (no GPU call here)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    line_out = reserve_line_stdout()
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if args.scaling is None:
         args.scaling = "weak" if world_env == 1 else "strong"
@@ -1053,6 +1232,9 @@ def main():
         STRONG["streams"] = args.strong_streams
         STRONG["balance"] = bool(args.strong_balance)
         STRONG["order"] = bool(args.strong_order)
+        STRONG["scene"] = args.strong_scene
+        STRONG["w"], STRONG["h"], STRONG["spp"] = (int(v) for v in args.strong_size.split("x"))
+        STRONG["name"] = f"{STRONG['scene']}-diffuse-{STRONG['w']}x{STRONG['h']}x{STRONG['spp']}spp"
         strong = strong_scaling(tracer, scenes, world, rank, args.strong_steps, 3, exact,
                                 with_roofline=args.scaling == "strong")
         log(f"[strong] {strong['workload']} n={world}: T1 {strong['t1_ms']} ms, Tn {strong['tn_ms']} ms, "
@@ -1072,7 +1254,7 @@ def main():
             line["extra_workloads"] = [{"workload": e["workload"], "value": e["value"]}
                                        for e in line.get("extra_workloads") or []]
             text = json.dumps(line, separators=(",", ":"))
-        print(text, flush=True)
+        print(text, file=line_out, flush=True)
         if LEARNED is not None:
             LEARNED.save(args.save_schedules)
             log(f"[schedules] saved {sum(len(v) for v in LEARNED.table.values())} to {args.save_schedules}")

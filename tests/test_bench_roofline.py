@@ -33,7 +33,7 @@ def profile(tmp_path, monkeypatch):
 def test_contract_fields_and_served_levels(profile):
     profile("w", l2=2.0e9, fabric=0.3e9, avg_ns=100_000)
     r = bench.roofline("w", 6.0e9, 0.1, 10 << 20, SCHED)   # 6 GB of algorithmic bytes in 0.1 ms: 60 TB/s
-    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == bench.HBM_PEAK_GBS
+    assert r["bound"] == "l2" and r["unit"] == "GB/s" and r["peak"] == bench.HBM_PEAK_GBS   # L2 serves 58 %
     assert r["achieved"] == pytest.approx(60000.0)
     assert r["frac"] == pytest.approx(60000.0 / bench.HBM_PEAK_GBS, rel=1e-3) and r["frac"] > 1.0
     assert "cache-resident" in r["note"]   # stated, not clamped
@@ -48,7 +48,7 @@ def test_contract_fields_and_served_levels(profile):
 def test_fabric_binding(profile):
     profile("w", l2=1.0e9, fabric=0.7e9, avg_ns=100_000)
     r = bench.roofline("w", 2.0e9, 0.1, 900 << 20, SCHED)
-    assert r["binding_level"] == "fabric" and r["bvh_exceeds_mall"]
+    assert r["binding_level"] == "fabric" and r["bvh_exceeds_mall"] and r["bound"] == "hbm"   # 81 % of 8.6 TB/s
     assert r["frac"] == pytest.approx(20000.0 / bench.HBM_PEAK_GBS, rel=1e-3)
 
 
@@ -84,3 +84,33 @@ def test_schedule_names():
     assert bench.schedule_name(2) == bench.SCHEDULES[2]
     assert bench.schedule_name(8 | (3 << 8)).endswith("spec_slack 4")
     assert bench.schedule_name(10 | (0 << 8)).endswith("no frontier tail")
+
+
+def test_latency_bound_when_every_level_is_lightly_served(profile):
+    """the bound is read from the served fractions — a launch whose levels
+    all serve under 25 % of their ceilings is latency-bound, not HBM-bound."""
+    profile("w", l2=1.0e9, fabric=0.1e9, avg_ns=100_000)    # L2: 10 TB/s of 34.5 = 29 %
+    r = bench.roofline("w", 2.0e9, 0.1, 10 << 20, SCHED)
+    assert r["served"]["l2"]["frac"] > bench.LATENCY_BOUND and r["bound"] == "l2"
+    profile("w", l2=0.5e9, fabric=0.1e9, avg_ns=100_000)    # 14 % of L2, 12 % of the fabric
+    r = bench.roofline("w", 2.0e9, 0.1, 10 << 20, SCHED)
+    assert max(v["frac"] for v in r["served"].values()) < bench.LATENCY_BOUND and r["bound"] == "latency"
+
+
+def test_kernel_bytes_give_their_own_frac(profile):
+    profile("w", l2=0.5e9, fabric=0.1e9, avg_ns=100_000)
+    r = bench.roofline("w", 9.0e9, 0.1, 10 << 20, SCHED, kernel_bytes_per_launch=6.0e9)
+    assert r["frac"] == pytest.approx(90000.0 / bench.HBM_PEAK_GBS, rel=1e-3)        # SURVEY 8(d), kept
+    assert r["kernel_frac"] == pytest.approx(60000.0 / bench.HBM_PEAK_GBS, rel=1e-3)
+    assert r["kernel_bytes_per_launch"] == int(6.0e9)
+
+
+@pytest.mark.parametrize("avg_ns,cited", [(100_000, True), (108_000, True), (115_000, False), (62_500, False)])
+def test_profile_at_another_speed_is_not_cited(profile, avg_ns, cited):
+    """a profile of the same schedule whose mean kernel time is outside
+    [0.9, 1.1] of this run's (the gloo rehearsal cited one at 0.625) is not cited."""
+    profile("w", l2=1.0e9, fabric=0.1e9, avg_ns=avg_ns)
+    r = bench.roofline("w", 2.0e9, 0.1, 10 << 20, SCHED)
+    assert (r["traffic"] is not None) == cited
+    if not cited:
+        assert "not cited" in r["profile"]["note"] and r["profile"]["kernel_ms_ratio"] == pytest.approx(avg_ns / 1e5)
