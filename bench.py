@@ -599,22 +599,30 @@ def cpu_baseline(batches, bufs, counted, threads, label, fast_results=None):
     workload: best of 5 after 1 warmup. Also checks the GPU results against it
     (parity on the bench input: closest hit bit-identical, any hit hit/miss-identical)
     and, given the fast-reciprocal mode's results, classifies their mismatches
-    (SURVEY §8(a) Note 3: tie / edge / other, tests/oracle_lib.classify_fast_rcp)."""
+    (SURVEY §8(a) Note 3: tie / edge / other, tests/oracle_lib.classify_fast_rcp). An
+    any-hit ray agrees when its hit/miss is the oracle's and, where its {id, t} differs,
+    the reported triangle passes the oracle's Woop test with exactly that t
+    (oracle_lib.invalid_hits: "valid hits", the reference's own any-hit contract)."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib as O
     nodes, woop, tri = bufs
     host = [(rb.rays.cpu().numpy(), not rb.need_closest_hit, rb.results_numpy()) for rb, _ in batches]
-    secs, agree, n = [], 0, 0
-    fast = {"rays": 0, "mismatch": 0, "tie": 0, "edge": 0, "other": 0, "any_hit_outcome_flips": 0} \
-        if fast_results is not None else None
+    secs, agree, n, any_checked = [], 0, 0, 0
+    fast = {"rays": 0, "mismatch": 0, "tie": 0, "edge": 0, "other": 0, "any_hit_outcome_flips": 0,
+            "any_hit_invalid": 0} if fast_results is not None else None
     for rep in range(6):
         total = 0.0
         for b, (rays, any_hit, gpu) in enumerate(host):
             res, _, s = O.trace(rays, nodes, woop, tri, any_hit=any_hit, threads=threads)
             total += s
             if rep == 0:
-                same = (gpu[:, 0] == -1) == (res[:, 0] == -1) if any_hit else \
-                    (gpu[:, 0] == res[:, 0]) & (gpu[:, 1] == res[:, 1])
+                same = (gpu[:, 0] == res[:, 0]) & (gpu[:, 1] == res[:, 1])
+                if any_hit:   # any valid hit is the reference's contract: re-verify every differing one
+                    diff = np.nonzero(~same)[0]
+                    bad = O.invalid_hits(rays, gpu, woop, tri, which=diff)
+                    same = (gpu[:, 0] == -1) == (res[:, 0] == -1)
+                    same[bad] = False
+                    any_checked += len(diff)
                 agree += int(same.sum())
                 n += len(rays)
                 if fast is not None:
@@ -625,6 +633,8 @@ def cpu_baseline(batches, bufs, counted, threads, label, fast_results=None):
                         fast["any_hit_outcome_flips"] += c["flips"]
                         fast["edge"] += c["edge"]
                         fast["other"] += c["other"]
+                        fd = np.nonzero((fr[:, 0] != res[:, 0]) | (fr[:, 1] != res[:, 1]))[0]
+                        fast["any_hit_invalid"] += len(O.invalid_hits(rays, fr, woop, tri, which=fd, rcp_ulps=1))
                     else:
                         c = O.classify_fast_rcp(rays, fr, res, woop, tri)
                         for k in ("mismatch", "tie", "edge", "other"):
@@ -637,7 +647,8 @@ def cpu_baseline(batches, bufs, counted, threads, label, fast_results=None):
            "cpu_model": cpu_model(), "seconds_best": round(best, 4),
            "sample": f"{label}: all {len(host)} batch(es), {rays} rays ({counted} counted), best of 5 after 1 "
                      f"warmup, {threads} threads, oracle/trace_oracle.c (same Compact2 bytes, same rays)",
-           "parity_exact_fraction": round(agree / max(1, n), 6)}
+           "parity_exact_fraction": round(agree / max(1, n), 6),
+           "any_hit_valid_hits_checked": any_checked}
     if fast is not None:
         fast["tie_fraction"] = round(fast["tie"] / max(1, fast["rays"]), 8)
         out["rcp_fast_parity"] = fast
@@ -1029,9 +1040,12 @@ def compact_roofline(rf):
 
 def compact_parity(cb, fast):
     out = {"exact_fraction": cb.get("parity_exact_fraction")} if cb else {}
+    if cb and cb.get("any_hit_valid_hits_checked"):
+        out["any_hit_valid_hits_checked"] = cb["any_hit_valid_hits_checked"]
     if fast and fast.get("parity"):
         fp = fast["parity"]
-        out["rcp_fast"] = {k: fp[k] for k in ("rays", "mismatch", "tie", "edge", "other", "any_hit_outcome_flips")}
+        out["rcp_fast"] = {k: fp[k] for k in ("rays", "mismatch", "tie", "edge", "other", "any_hit_outcome_flips",
+                                              "any_hit_invalid") if k in fp}
     return out
 
 

@@ -29,6 +29,8 @@ def lib():
         L.oracle_woop_hit.argtypes = [vp, vp, i64, i64, C.c_float, C.POINTER(C.c_float)]
         L.oracle_woop_hit_rcp.restype = C.c_int
         L.oracle_woop_hit_rcp.argtypes = [vp, vp, i64, i64, C.c_float, C.c_int, C.POINTER(C.c_float)]
+        L.oracle_check_hits.restype = i64
+        L.oracle_check_hits.argtypes = [vp, vp, vp, i64, vp, i64, vp, C.c_int, vp]
         L.oracle_brute_force.restype = None
         L.oracle_brute_force.argtypes = [vp, vp, i64, C.c_int, vp, i64, vp]
         L.oracle_tri_colors.restype = None
@@ -75,6 +77,23 @@ def woop_hit_rcp(ray, woop, slot, tmax, rcp_ulps):
     hit = lib().oracle_woop_hit_rcp(_p(ray), _p(woop), woop.nbytes, int(slot), float(tmax), int(rcp_ulps),
                                     C.byref(t))
     return bool(hit), float(t.value)
+
+
+def invalid_hits(rays, res, woop, tri_index, which=None, rcp_ulps=0):
+    """Indices (into rays) of reported results that are not genuine: a hit {id, t} no
+    triangle with that triIndex reproduces under the Woop test of the ray against its
+    (tmin, tmax) with 1/Dz within rcp_ulps ulps of 1/Dz, or a miss whose t is not the
+    ray's tmax (oracle_check_hits). which: the rays to check (default: all)."""
+    rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)
+    res = np.ascontiguousarray(res, np.int32).reshape(-1, 4)
+    woop = np.ascontiguousarray(woop).view(np.int32)
+    tri = np.ascontiguousarray(tri_index, np.int32)
+    idx = np.arange(len(rays), dtype=np.int64) if which is None else np.ascontiguousarray(which, np.int64)
+    ok = np.zeros(len(idx), np.uint8)
+    if len(idx):
+        lib().oracle_check_hits(_p(rays), _p(res), _p(idx), len(idx), _p(woop), woop.nbytes, _p(tri), int(rcp_ulps),
+                                _p(ok))
+    return idx[ok == 0]
 
 
 def _ulps(a, b):

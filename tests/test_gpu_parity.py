@@ -55,22 +55,18 @@ def ulp_diff(a_bits, b_bits):
     return np.abs(a - b)
 
 
-def assert_valid_hits(rays, res, oracle_res, bufs):
-    """Every differing any-hit result is a genuine hit the oracle's Woop test reproduces."""
+def assert_valid_hits(rays, res, oracle_res, bufs, rcp_ulps=0):
+    """Every any-hit result that differs from the oracle's is genuine: hit/miss
+    identical, and each differing hit a triangle whose Woop test the oracle reproduces with
+    exactly the reported t (oracle_lib.invalid_hits, one C pass over all of them; rcp_ulps 1
+    for the fast-reciprocal mode, whose 1/Dz may be one ulp off). Returns the rays checked."""
     nodes, woop, tri = bufs
-    diff = np.nonzero((res[:, 0] != oracle_res[:, 0]) | (res[:, 1] != oracle_res[:, 1]))[0]
     assert np.array_equal(res[:, 0] == -1, oracle_res[:, 0] == -1), "hit/miss differs"
-    woop4 = woop.reshape(-1, 4)
-    for i in diff[:2000]:
-        # find a woop slot holding triangle res[i,0] whose Woop test gives exactly res t
-        cand = np.nonzero((tri == res[i, 0]) & (woop4[:, 0] != np.int32(-2147483648)))[0]
-        ok = False
-        for s in cand:
-            hit, t = O.woop_hit(rays[i], woop, s, float(rays[i][7]))
-            if hit and np.float32(t).view(np.int32) == res[i, 1]:
-                ok = True
-                break
-        assert ok, f"ray {i}: GPU any-hit ({res[i, 0]}, {res[i, 1]}) is not a valid hit"
+    diff = np.nonzero((res[:, 0] != oracle_res[:, 0]) | (res[:, 1] != oracle_res[:, 1]))[0]
+    bad = O.invalid_hits(rays, res, woop, tri, which=diff, rcp_ulps=rcp_ulps)
+    assert len(bad) == 0, (f"{len(bad)} of {len(diff)} differing any-hit results are not valid hits, e.g. ray "
+                           f"{bad[0]}: GPU ({res[bad[0], 0]}, {res[bad[0], 1]}) oracle {tuple(oracle_res[bad[0], :2])}")
+    return len(diff)
 
 
 # ---------------------------------------------------------------- known answers

@@ -3,7 +3,9 @@ code (bench.Batches / bench.strong_scaling's Renderer batches) and compared with
 the CPU oracle ray by ray:
 
   configs[1] bunny primary 1024x768       test_gpu_parity.py::test_full_size_bunny_primary_1024x768
-  configs[2] conference AO 640x480        any hit: hit/miss identical, every hit a valid Woop hit
+  configs[2] conference AO 640x480        any hit: hit/miss identical, every hit that differs from the
+                                          oracle's re-verified as a Woop hit with exactly its t (exact and
+                                          fast reciprocal)
   configs[3] sponza diffuse, 2 bounces    both bounce batches: closest hit bit-identical
   configs[4] hairball (6 469 561 tris)    diffuse 640x480 (+ per-lane counters), 1920x1080, and the
                                           16.6 M-ray 1920x1080x8spp strong-scaling RayBuffer
@@ -47,9 +49,13 @@ def trace_and_compare(tracer, rb, bufs, threads, counters=False):
     want, st, _ = O.trace(rays, *bufs, any_hit=any_hit, stats=counters, threads=threads)
     tracer.trace_batch(rb, exact_rcp=True)
     got = rb.results_numpy()
-    if any_hit:
+    if any_hit:   # hit/miss identical; every hit that differs a genuine Woop hit with its t
         assert np.array_equal(got[:, 0] == -1, want[:, 0] == -1), "any-hit hit/miss differs"
         assert np.array_equal(got[want[:, 0] == -1, 1], want[want[:, 0] == -1, 1])
+        diff = np.nonzero((got[:, 0] != want[:, 0]) | (got[:, 1] != want[:, 1]))[0]
+        bad = O.invalid_hits(rays, got, bufs[1], bufs[2], which=diff)
+        assert len(bad) == 0, f"{len(bad)} of {len(diff)} differing any hits are not valid hits, e.g. ray {bad[:5]}"
+        print(f"any hit: {len(diff)} of {len(rays)} rays report another valid hit than the oracle's; all genuine")
     else:
         bad = np.nonzero((got[:, 0] != want[:, 0]) | (got[:, 1] != want[:, 1]))[0]
         assert len(bad) == 0, f"{len(bad)} of {len(rays)} rays differ, e.g. ray {bad[:5]}"
@@ -247,7 +253,12 @@ def test_fast_rcp_mismatches_are_classified(env, name):
             total["rays"] += len(rays)
             total["edge"] += c["edge"]
             total["other"] += c["other"]
-            print(name, c)
+            # every hit or miss that differs from the oracle's is genuine under v_rcp_f32's one-ulp
+            # bound on 1/Dz: a Woop hit with exactly its t, or a miss with t = tmax
+            diff = np.nonzero((got[:, 0] != want[:, 0]) | (got[:, 1] != want[:, 1]))[0]
+            bad = O.invalid_hits(rays, got, bufs[1], bufs[2], which=diff, rcp_ulps=1)
+            assert len(bad) == 0, f"{len(bad)} of {len(diff)} differing fast any-hit results are not genuine"
+            print(name, c, f"{len(diff)} differing results, all genuine")
             continue
         c = O.classify_fast_rcp(rays, got, want, bufs[1], bufs[2])
         assert c["unclassified"] == 0

@@ -82,6 +82,34 @@ def test_any_hit_agrees_with_closest_on_hit_or_miss():
     assert (anyh[hit, 1].view(np.float32) >= closest[hit, 1].view(np.float32)).all()
 
 
+def test_invalid_hits_accepts_genuine_results_and_rejects_altered_ones():
+    """oracle_lib.invalid_hits (the batch valid-hit check of the GPU any-hit and fast-rcp
+    tests): every result the oracle itself reports is genuine — closest and
+    any hit, hits and misses — and one ulp on a hit's t, another triangle id, or a miss
+    whose t is not tmax is not."""
+    scene = mrt.Scene.synthetic("random", 3000, 5)
+    nodes, woop, tri = mrt.Bvh.build(scene).buffers()
+    cam, _ = scene.camera()
+    rays, _ = mrt.primary_rays(cam, 64, 48)
+    for any_hit in (False, True):
+        res, _, _ = O.trace(rays, nodes, woop, tri, any_hit=any_hit)
+        assert len(O.invalid_hits(rays, res, woop, tri)) == 0
+    hits = np.nonzero(res[:, 0] != -1)[0][:50]
+    misses = np.nonzero(res[:, 0] == -1)[0][:50]
+    assert len(hits) == 50 and len(misses) == 50
+    bad_t = res.copy()
+    bad_t[hits, 1] += 1
+    assert np.array_equal(O.invalid_hits(rays, bad_t, woop, tri, which=hits), hits)
+    bad_id = res.copy()
+    bad_id[hits, 0] += 1   # the neighbouring triangle (never the same t bits on these rays)
+    assert len(O.invalid_hits(rays, bad_id, woop, tri, which=hits)) == 50
+    bad_miss = res.copy()
+    bad_miss[misses, 1] = np.float32(1.0).view(np.int32)
+    assert np.array_equal(O.invalid_hits(rays, bad_miss, woop, tri, which=misses), misses)
+    # with 1/Dz allowed one ulp off (the fast mode's bound) a one-ulp t may be genuine
+    assert len(O.invalid_hits(rays, bad_t, woop, tri, which=hits, rcp_ulps=1)) < 50
+
+
 def test_threads_do_not_change_results():
     scene = mrt.Scene.synthetic("mori", 0, 1)
     nodes, woop, tri = mrt.Bvh.build(scene).buffers()
