@@ -4,7 +4,8 @@
 #   test[=EXPR]     pytest -m gpu (with -k EXPR)                   -> gpurun_out/pytest_gpu.log
 #   smoke           __graft_entry__.smoke()                        -> gpurun_out/smoke.log
 #   bench[=ARGS]    bench.py ARGS (commas become spaces)           -> gpurun_out/bench.json, bench_detail.json
-#   gloo            the N=2 flow, two gloo ranks on the one GPU    -> gpurun_out/bench_gloo2.json
+#   gloo            the N=2 flow, two gloo ranks on the one GPU, started by bench.py itself -> gpurun_out/bench_gloo2.json
+#   gloorun         the same under torch.distributed.run           -> gpurun_out/bench_gloorun2.json
 #   tune            steady-state schedules of the bench workloads  -> gpurun_out/tuned_schedules.json
 #   profile=TAG     rocprofv3 kernel stats + PMC summaries of the bench workloads (PROF_WL overrides the list)
 #                                                                  -> gpurun_out/profiles/TAG_*
@@ -32,11 +33,15 @@ for step in "$@"; do
     bench)
       timeout -k 10 600 python bench.py ${arg//,/ } --detail-out $O/bench_detail.json > $O/bench.json 2> $O/bench.err || fail bench $O/bench.err
       grep -E "\[(head|extra|strong|line)\]" $O/bench.err ;;
-    gloo)
+    gloo)   # bench.py starts its two ranks itself (no launcher), as `python bench.py --gpus N` would
+      timeout -k 10 600 python bench.py --gpus 2 --dist-backend gloo --steps 10 --detail-out $O/bench_gloo2_detail.json \
+        > $O/bench_gloo2.json 2> $O/bench_gloo2.err || fail "gloo rehearsal" $O/bench_gloo2.err
+      grep -E "\[(head|strong|launch)\]" $O/bench_gloo2.err ;;
+    gloorun)   # the same under torch.distributed.run (the driver's N>1 launch)
       timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
-        bench.py --gpus 2 --dist-backend gloo --steps 10 --detail-out $O/bench_gloo2_detail.json > $O/bench_gloo2.json 2> $O/bench_gloo2.err \
-        || fail "gloo rehearsal" $O/bench_gloo2.err
-      grep -E "\[(head|strong)\]" $O/bench_gloo2.err ;;
+        bench.py --gpus 2 --dist-backend gloo --steps 10 --detail-out $O/bench_gloorun2_detail.json > $O/bench_gloorun2.json 2> $O/bench_gloorun2.err \
+        || fail "gloo rehearsal (torchrun)" $O/bench_gloorun2.err
+      grep -E "\[(head|strong)\]" $O/bench_gloorun2.err ;;
     tune)
       rm -f $O/tuned_schedules.json
       W=""; for w in $BENCH_WL; do [ $w = hairball-diffuse-1920x1080 ] || W="$W --workload $w"; done
