@@ -28,6 +28,7 @@ struct Workspace;
 struct mrt_tracer {
     int device = 0;
     int numCUs = 0;
+    int numXccs = 1;   // XCDs of the device (partition): the per-XCD queue candidate's queue count
     std::mutex mu;
 
     // Bound Compact2 BVH (borrowed device pointers).
@@ -78,7 +79,8 @@ struct mrt_tracer {
 struct TuneState {
     // Stage 1: kSchedules ray-distribution schedules; stage 2: the stage-1 winner
     // with the speculation slack at 4 and 6, without the frontier tail (with it if the
-    // tracer's default is off), and with 16 lane groups (candidates kSchedules .. + 3).
+    // tracer's default is off), with 16 lane groups, and with 2 lane groups at slack 6
+    // (candidates kSchedules .. kSchedules + kStage2 - 1).
     static constexpr int kSchedules = 8;
     static constexpr int kStage2 = 5;
     static constexpr int kCandidates = kSchedules + kStage2;
@@ -92,7 +94,8 @@ struct TuneState {
     int stage1 = -1;     // the stage-1 winner, once every schedule has kSamples samples
     int locked = -1;     // the chosen candidate, once stage 2's have kSamples samples too
     void* stream = nullptr;          // the stream this batch size was first launched on
-    bool multiStream = false;        // launched on several streams: keeps the fixed rule
+    bool multiStream = false;        // launched on several streams: not explored (settled schedule or the rule)
+    bool inherited = false;          // took a nearby batch size's schedule (kTuneInherit): not exported
     struct Pending {
         hipEvent_t start = nullptr, stop = nullptr;
         int cand = -1;   // -1 = slot free
@@ -217,6 +220,7 @@ mrt_launch_cfg default_cfg() {
     c.tail_lanes = kDefaultTailLanes;
     c.queue_shared = 0;
     c.queue_block = 0;
+    c.queue_xcc_mask = 0;
     return c;
 }
 
@@ -229,7 +233,8 @@ bool valid_cfg(const mrt_launch_cfg& c) {
            c.static_rounds >= 1 && c.static_rounds <= 64 && (c.autotune == 0 || c.autotune == 1) &&
            c.tail_lanes >= 0 && c.tail_lanes <= 16 &&
            c.queue_shared >= 0 && c.queue_shared <= 100 && c.queue_block >= 0 && c.queue_block <= (1 << 20) &&
-           (c.queue_block & (c.queue_block - 1)) == 0 && (c.queue_block == 0 || c.queue_block >= 64);
+           (c.queue_block & (c.queue_block - 1)) == 0 && (c.queue_block == 0 || c.queue_block >= 64) &&
+           c.queue_xcc_mask >= 0 && c.queue_xcc_mask <= 15;
 }
 
 // The frontier tail runs in the exact 4-wide kernels whose leaf refs carry counts.
@@ -486,12 +491,12 @@ constexpr int kXcdQueueBlock = 8192;
 constexpr int kXcdQueueShared = 0;
 constexpr int kXcdQueueThreshold = 56;
 
-mrt_launch_cfg tune_candidate(const mrt_launch_cfg& base, int c, int stage1) {
+mrt_launch_cfg tune_candidate(const mrt_tracer* t, const mrt_launch_cfg& base, int c, int stage1) {
     if (c >= TuneState::kSchedules) {
         // stage 2: the stage-1 winner, the wave turning to its leaves once <= 4 (6) lanes
         // still search, with the frontier tail toggled, or with its lanes taking rays from 16
         // distant parts of each strided chunk (only for knobs the caller left at their defaults)
-        mrt_launch_cfg x = tune_candidate(base, stage1, stage1);
+        mrt_launch_cfg x = tune_candidate(t, base, stage1, stage1);
         const int k = c - TuneState::kSchedules;
         if (k < 2 && base.spec_slack == kDefaultSpecSlack) x.spec_slack = k == 0 ? 4 : 6;
         if (k == 2 && base.tail_lanes == kDefaultTailLanes) x.tail_lanes = kDefaultTailLanes ? 0 : kTunedTailLanes;
@@ -523,7 +528,7 @@ mrt_launch_cfg tune_candidate(const mrt_launch_cfg& base, int c, int stage1) {
                   // Infinity Cache (hairball 2 M rays: 0.630 -> 0.547 ms, fabric bytes 1.07 -> 0.74 GB at
                   // 4096-ray blocks, profiles/round4_queue_ab.txt; 8192: 1.4 % faster again and the
                   // strong-scaling shards' best, round4_order_sweep.txt)
-            x.num_queues = 8;
+            x.num_queues = std::max(1, std::min(t->numXccs, mrt::kMaxQueues));   // one per XCD, never more
             x.queue_block = kXcdQueueBlock;
             x.queue_shared = kXcdQueueShared;
             x.fetch_threshold = kXcdQueueThreshold;
@@ -641,6 +646,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
                 bestGap = gap;
                 tune->stage1 = kv.second->stage1;
                 tune->locked = kv.second->locked;
+                tune->inherited = true;
             }
             t->tunes[key] = tune;
         }
@@ -672,7 +678,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
                 MRT_HIP(hipEventCreateWithFlags(&slot->stop, mrt::kTimingEventFlags));
             }
         }
-        cfg = tune_candidate(cfg, cand, tune->stage1);
+        cfg = tune_candidate(t, cfg, cand, tune->stage1);
     }
     v.tail = with_tail(t, v, cfg);   // a tuned candidate may run without the tail
     const int blocks = grid_blocks(t, cfg, v, numRays, &perCU);
@@ -706,6 +712,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     a.stackCap = stackCap;
     a.stackBound = wide ? t->wideStackBound : stackCap - 1;
     a.tailLanes = cfg.tail_lanes;
+    a.xccMask = cfg.queue_xcc_mask;
     a.queues = ws->queues;
     a.spill = ws->spill;
     // The blocking call counts this launch's overflows in a slot of its own; the
@@ -834,11 +841,15 @@ int mrt_tracer_create(int device, mrt_tracer** out) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(MRT_ERR_NO_DEVICE, "no HIP device visible");
     if (device < 0 || device >= n) return fail(MRT_ERR_INVALID_ARG, "device index out of range");
-    int cus = 0;
+    int cus = 0, xccs = 0;
     MRT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    // XCDs of this device (partition): the HIP attribute, else 32 CUs per MI355X XCD
+    if (hipDeviceGetAttribute(&xccs, hipDeviceAttributeNumberOfXccs, device) != hipSuccess || xccs <= 0)
+        xccs = std::max(1, cus / 32);
     mrt_tracer* t = new mrt_tracer();
     t->device = device;
     t->numCUs = cus;
+    t->numXccs = std::max(1, std::min(xccs, mrt::kMaxQueues));
     t->cfg = default_cfg();
     *out = t;
     return MRT_OK;
@@ -913,6 +924,9 @@ int mrt_tracer_set_config(mrt_tracer* t, const mrt_launch_cfg* cfg) {
     if (c.static_rounds == 0) c.static_rounds = d.static_rounds;
     if (c.autotune < 0) c.autotune = d.autotune;
     if (c.tail_lanes < 0) c.tail_lanes = d.tail_lanes;
+    if (c.queue_shared < 0) c.queue_shared = d.queue_shared;
+    if (c.queue_block < 0) c.queue_block = d.queue_block;
+    if (c.queue_xcc_mask < 0) c.queue_xcc_mask = d.queue_xcc_mask;
     if (!valid_cfg(c)) return fail(MRT_ERR_INVALID_ARG, "launch config out of range");
     std::lock_guard<std::mutex> lock(t->mu);
     t->cfg = c;
@@ -949,7 +963,8 @@ int mrt_tracer_tune_export(const mrt_tracer* t, mrt_tuned_schedule* out, int32_t
     std::lock_guard<std::mutex> lock(const_cast<mrt_tracer*>(t)->mu);
     int n = 0;
     for (const auto& kv : t->tunes) {
-        if (kv.second->locked < 0) continue;
+        // inherited entries were tuned for another batch (size and ray distribution): not saved as tuned
+        if (kv.second->locked < 0 || kv.second->inherited) continue;
         if (n < capacity)
             out[n] = mrt_tuned_schedule{kv.first.first, kv.first.second,
                                         kv.second->locked | (std::max(0, kv.second->stage1) << 8), MRT_TUNE_VERSION};

@@ -93,14 +93,16 @@ def shard_spans(n: int, world: int, rank: int, block: int = 0, owners=None, prio
         if len(pr) != nblocks:
             raise ValueError(f"shard_spans: {len(pr)} block priorities for {nblocks} blocks of {block} rays")
         mine = mine[np.argsort(-pr[mine], kind="stable")]
-    spans: list[tuple[int, int]] = []
-    for i in mine:
-        a, b = int(i) * block, min(n, (int(i) + 1) * block)
-        if spans and spans[-1][1] == a:
-            spans[-1] = (spans[-1][0], b)
-        else:
-            spans.append((a, b))
-    return spans
+    if len(mine) == 0:
+        return []
+    # the blocks' ranges, adjacent ones merged (vectorised: a 16.6 M-ray buffer has 16 k blocks)
+    starts = mine.astype(np.int64) * block
+    ends = np.minimum(n, starts + block)
+    first = np.ones(len(mine), bool)
+    first[1:] = starts[1:] != ends[:-1]
+    heads = np.flatnonzero(first)
+    last = np.append(heads[1:] - 1, len(mine) - 1)
+    return list(zip(starts[heads].tolist(), ends[last].tolist()))
 
 
 def spans_index(spans, device=None) -> torch.Tensor:

@@ -76,7 +76,12 @@ typedef struct mrt_launch_cfg {
                                   20 of 32, kepler_dynamic_fetch.cu:48). Static strided rounds ignore it   */
     int32_t num_queues;        /* -1 (default) = static strided rounds, no atomics; 1..8 = the reference's
                                   dynamic fetch: a static first round, then one atomic per wave refill
-                                  on the queue of the wave's XCD (xcc % num_queues), no stealing      */
+                                  on the queue of the wave's XCD (xcc % num_queues), no stealing of rays
+                                  from a served queue; a queue no wave has taken from when a wave's own
+                                  queue is dry (an XCD without workgroups of the launch, e.g. a CPX/DPX
+                                  partition) is adopted by that wave, so every ray is traced whatever
+                                  the placement. The autotuner's per-XCD candidate uses one queue per
+                                  XCD of the device (hipDeviceAttributeNumberOfXccs)                   */
     int32_t lds_stack;         /* traversal-stack entries per lane kept in LDS: 8, 16 or 32       */
     int32_t lane_groups;       /* strided mode: a wave's 64 lanes take rays from this many (1..64, power of
                                   two) distant sub-ranges of the batch instead of 64 consecutive rays */
@@ -103,7 +108,10 @@ typedef struct mrt_launch_cfg {
                                   after one untimed round of them; the median ranks them and a candidate
                                   replaces the fixed rule (stage 1) or the stage-1 winner (stage 2) only
                                   when 3 % faster. A new batch size within 1/32 of a settled one (same
-                                  variant) takes the nearest settled schedule without exploring. A batch
+                                  variant) takes the nearest settled schedule without exploring —
+                                  a schedule tuned on another ray distribution of that size (e.g. a
+                                  primary batch's for a diffuse one over the same BVH); such inherited
+                                  entries are not exported by mrt_tracer_tune_export. A batch
                                   size launched on more than one stream is not explored: it runs its settled
                                   schedule if it has one, else the fixed rule; reset by bind and set_config (default 1; mrt_tracer_tune_export /
                                   _import save and restore the choices). 0 = the fixed rule only; -1 = default */
@@ -115,10 +123,15 @@ typedef struct mrt_launch_cfg {
                                   default 16; -1 = default; the autotuner tries 0 when left at the default) */
     int32_t queue_shared;      /* num_queues > 1: this percentage of the batch's rays (its end) goes to one
                                   shared queue that a wave takes from once its XCD's queue is dry; the
-                                  rest is dealt in per-XCD contiguous shares (0..100; default 0)       */
+                                  rest is dealt in per-XCD contiguous shares (0..100; default 0; -1 =
+                                  default)                                                             */
     int32_t queue_block;       /* num_queues > 1: 0 = each queue's share is contiguous; a power of two >= 64 =
                                   the shares are this many rays' blocks dealt cyclically (block i to queue
-                                  i mod num_queues), so every XCD samples the whole frame              */
+                                  i mod num_queues), so every XCD samples the whole frame (default 0;
+                                  -1 = default)                                                        */
+    int32_t queue_xcc_mask;    /* test hook, 0 = off (default; -1 = default): 1..15 = a wave takes from queue
+                                  (XCC_ID & mask) % num_queues, so with mask 3 and 8 queues, queues 4..7
+                                  have no waves of their own (the unserved-queue sweep must trace them) */
 } mrt_launch_cfg;
 
 /* Per-launch statistics reported back to the host (optional). */
@@ -134,7 +147,11 @@ typedef struct mrt_trace_info {
     int32_t stack_overflows;   /* entries pushed past stack_capacity in this launch (then the call returns
                                   MRT_ERR_STACK_OVERFLOW; 0 for any SBVH of depth <= 64)            */
     int32_t node_bytes;        /* bytes per node the launch read: 64 (Compact2 or quantized 4-wide), 128 */
-    int32_t autotune_candidate; /* cfg.autotune: the schedule candidate this launch used (0..9), else -1 */
+    int32_t autotune_candidate; /* cfg.autotune: the schedule candidate this launch used, else -1 (the fixed
+                                  rule): 0..7 a ray-distribution schedule; 8..12 a stage-2 modifier of
+                                  the stage-1 schedule s, encoded as modifier | s << 8 (8/9: spec_slack
+                                  4/6, 10: the frontier tail toggled, 11: 16 lane groups, 12: 2 lane
+                                  groups at spec_slack 6; bench.py schedule_name spells them out)    */
     int32_t autotune_locked;   /* 1 once the batch size's schedule is chosen                      */
     int32_t stack_capacity;    /* stack entries (sentinel included) the launch had: 64 = the reference's
                                   for the binary order; the wide orders get the bound tree's worst case

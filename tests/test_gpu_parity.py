@@ -234,6 +234,52 @@ def test_launch_configs_do_not_change_results(tracer, cfg):
         tracer.set_config(**saved)
 
 
+@pytest.mark.parametrize("cfg", [dict(num_queues=8, queue_xcc_mask=3), dict(num_queues=8, queue_xcc_mask=1),
+                                 dict(num_queues=8, queue_xcc_mask=3, queue_shared=10),
+                                 dict(num_queues=5, queue_xcc_mask=3), dict(num_queues=8, queue_xcc_mask=0)],
+                         ids=lambda c: ",".join(f"{k}={v}" for k, v in c.items()))
+def test_queues_without_waves_are_still_traced(tracer, cfg):
+    """with per-XCD queues a wave takes from queue XCC_ID % num_queues; on a
+    device or partition where some queue gets no waves (CPX/DPX, a placement that skips an
+    XCD) its rays must still be traced. The test hook queue_xcc_mask masks XCC_ID so that
+    only queues 0..mask have waves (mask 1: a quarter of the 8 queues); the queues past the
+    first static round hold most of the 307 200-ray batch (4 waves/CU = 65 536 static rays,
+    1 024-ray blocks). Every ray equals the oracle, closest hit and per-lane counters."""
+    bufs, rays, any_hit, want, st = scene_setup("conference", 640, 480, "diffuse")
+    saved = tracer.config()
+    try:
+        tracer.set_config(queue_block=1024, fetch_threshold=56, waves_per_cu=4, autotune=0, **cfg)
+        res, _ = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=True)
+        assert np.array_equal(res[:, :2], want[:, :2])
+        assert tracer.last_info["num_queues"] == cfg["num_queues"]
+        res, gst = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=False, stats=True)
+        assert np.array_equal(res[:, :2], want[:, :2]) and np.array_equal(gst[:, :3], st[:, :3])
+    finally:
+        tracer.set_config(**saved)
+
+
+def test_per_xcd_candidate_uses_one_queue_per_xcd(tracer):
+    """The autotuner's per-XCD candidate (2) sizes its queues from the device's XCD count
+    (hipDeviceAttributeNumberOfXccs), never more: 8 on an SPX MI355X."""
+    from mrt.tracer import GpuBvh, RayBuffer
+    bufs, rays, any_hit, want, _ = scene_setup("conference", 640, 480, "diffuse")
+    saved = tracer.config()
+    try:
+        tracer.set_config(autotune=1)
+        tracer.set_bvh(GpuBvh(bufs))
+        rb = RayBuffer(rays, need_closest_hit=True)
+        seen = {}
+        for _ in range(40):   # the exploring launches cycle through the eight stage-1 schedules
+            tracer.trace_batch(rb, exact_rcp=True)
+            seen[tracer.last_info["autotune_candidate"]] = tracer.last_info["num_queues"]
+        assert 2 in seen
+        cus = torch.cuda.get_device_properties(0).multi_processor_count
+        assert 1 <= seen[2] <= 8 and seen[2] == min(8, max(1, cus // 32))
+        assert np.array_equal(rb.results_numpy()[:, :2], want[:, :2])
+    finally:
+        tracer.set_config(**saved)
+
+
 def test_deep_stacks_and_rebinding(tracer):
     """An 8-entry LDS ring (deep stacks spill to the slab) and a re-bound BVH."""
     saved = tracer.config()
