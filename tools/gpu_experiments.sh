@@ -22,6 +22,11 @@
 #   deal_rot     ordered shards: block-cyclic deal vs the deal rotated by one rank per round
 #   ao_knobs     Mori / Fairy AO under launch knobs the autotuner does not explore
 #   timeline_shard  per-ray timeline of shard 0, live first vs frame order (variants/tailtl build)
+# Round-5 experiments:
+#   r5_guard     the unserved-queue sweep's cost: this tree vs the round-4 kernel (variants/r4, built at
+#                d775aa0 by tools/build_variant.sh r4 "" d775aa0) on the saved schedules  -> profiles/round5_guard_ab.txt
+#   r5_hb640     hairball diffuse 640x480: global vs per-XCD queues x refill x waves x slack
+#   r5_ao        Mori / Fairy AO: grid size and the frontier tail
 # Usage: gpurun -- 'bash tools/gpu_experiments.sh order order2'
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -187,6 +192,32 @@ print('block $B balance $BAL T1', d['t1_ms'], 'one-stream', d.get('one_stream_ms
       timeout -k 10 600 python -u tools/ab.py --rounds 7 --launches 30 --workload mori-ao-640x480 --workload fairy-ao-640x480 $V \
         > $O/ab_ao.txt 2> $O/ab_ao.err || fail ab $O/ab_ao.err
       cat $O/ab_ao.txt ;;
+    r5_guard)
+      timeout -k 10 600 python -u tools/ab.py --rounds 11 --launches 30 --workload hairball-diffuse-1920x1080 \
+        --workload bunny-primary-1024x768 --workload hairball-diffuse-640x480 --workload conference-ao-640x480 \
+        --variant 'lib:{"saved":1}' --variant 'variants/r4:{"saved":1}' > $O/ab_guard.txt 2> $O/ab_guard.err || fail ab $O/ab_guard.err
+      cat $O/ab_guard.txt ;;
+    r5_hb640)
+      V='--variant lib:{"saved":1}'
+      for W in 12 16; do for T in 40 48 56; do
+        V="$V --variant lib:{\"autotune\":0,\"num_queues\":1,\"fetch_threshold\":$T,\"waves_per_cu\":$W}"
+      done; done
+      for B in 1024 4096; do for W in 12 16; do
+        V="$V --variant lib:{\"autotune\":0,\"num_queues\":8,\"fetch_threshold\":48,\"waves_per_cu\":$W,\"queue_block\":$B}"
+      done; done
+      V="$V --variant lib:{\"autotune\":0,\"num_queues\":1,\"fetch_threshold\":48,\"waves_per_cu\":12,\"spec_slack\":4}"
+      V="$V --variant lib:{\"autotune\":0,\"num_queues\":1,\"fetch_threshold\":48,\"waves_per_cu\":12,\"tail_lanes\":8}"
+      V="$V --variant lib:{\"autotune\":0,\"num_queues\":1,\"fetch_threshold\":48,\"waves_per_cu\":12,\"static_rounds\":2}"
+      timeout -k 10 600 python -u tools/ab.py --rounds 9 --launches 30 --workload hairball-diffuse-640x480 $V \
+        > $O/ab_hb640.txt 2> $O/ab_hb640.err || fail ab $O/ab_hb640.err
+      cat $O/ab_hb640.txt ;;
+    r5_ao)
+      V='--variant lib:{"saved":1}'
+      for W in 4 6 8 12 16 20 24 32; do V="$V --variant lib:{\"autotune\":0,\"waves_per_cu\":$W}"; done
+      V="$V --variant lib:{\"autotune\":0,\"tail_lanes\":0}"
+      timeout -k 10 600 python -u tools/ab.py --rounds 7 --launches 30 --workload mori-ao-640x480 --workload fairy-ao-640x480 $V \
+        > $O/ab_ao5.txt 2> $O/ab_ao5.err || fail ab $O/ab_ao5.err
+      cat $O/ab_ao5.txt ;;
     *) echo "unknown experiment $exp"; exit 2 ;;
   esac
 done
