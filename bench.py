@@ -113,7 +113,7 @@ EXTRA_N1 = ["bunny-primary-640x480", "conference-ao-640x480", "sponza-diffuse-64
 # min_launches: a shard is cut into at least this many launches (alternating over two streams).
 STRONG = {"name": "hairball-diffuse-1920x1080x8spp", "scene": "hairball", "w": 1920, "h": 1080, "spp": 8,
           "max_batch": 1 << 21, "min_launches": 1, "block": 1 << 10, "streams": 2, "balance": False,
-          "order": True}
+          "order": 1}
 STRONG_PROJECT = (2, 4, 8)   # N=1 only: rank counts whose per-rank shards are timed on the one GPU
 
 
@@ -864,32 +864,46 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
     whole buffer alone, same run; then the {id, t} gather to rank 0, checked
     against the single-GPU results."""
     import torch
-    from mrt.dist import (balance_blocks, block_weights, gather_results, local_rays, shard_launches, shard_spans,
-                          spans_index)
+    from mrt.dist import (balance_blocks, block_sums, block_weights, gather_results, local_rays, shard_launches,
+                          shard_spans, spans_index)
     from mrt.raygen import RAY_DIFFUSE
-    from mrt.renderer import Renderer
+    from mrt.renderer import GlibcRand, Renderer
     from mrt.tracer import RayBuffer
     cfg = STRONG
     e = scenes.get(cfg["scene"])
     bind(tracer, e["gbvh"])
     cam, _ = e["scene"].camera()
-    r = Renderer(tracer, e["scene"], max_batch=cfg["max_batch"], exact_rcp=True)
-    r.set_params(RAY_DIFFUSE, cfg["spp"])
-    r.begin_frame(cam, cfg["w"], cfg["h"])
-    counted = r.total_num_rays()
-    parts = [b for b, _ in r.batches()]
-    n = sum(b.size for b in parts)
-    big = RayBuffer(torch.cat([b.rays for b in parts]), need_closest_hit=True)
-    del parts, r
+    rnd = GlibcRand()   # the reference's rand() sequence: this frame's batch seeds, then the next frame's
+
+    def frame():
+        r = Renderer(tracer, e["scene"], max_batch=cfg["max_batch"], exact_rcp=True, rand=rnd)
+        r.set_params(RAY_DIFFUSE, cfg["spp"])
+        r.begin_frame(cam, cfg["w"], cfg["h"])
+        parts = [b for b, _ in r.batches()]
+        return RayBuffer(torch.cat([b.rays for b in parts]), need_closest_hit=True), r.total_num_rays()
+
+    big, counted = frame()
+    n = big.size
 
     # Blocks dealt by live-ray count (balance_blocks) or cyclically, and within a shard
-    # in frame order or costly (live) blocks first (order): every rank computes the same
-    # deal from the buffer's tmax column (one reduction, brought to the host once so
-    # that no later shard_spans call syncs the device — the timed gather calls it
-    # world + 1 times).
+    # in frame order (order 0), live blocks first (1) or costly blocks first (2): every rank
+    # computes the same deal (one reduction, brought to the host once so that no later
+    # shard_spans call syncs the device — the timed gather calls it world + 1 times).
+    # Order 2's cost is what a renderer knows from the frame before: the NEXT frame of the
+    # same view (the following rand() seeds: the same pixels, other sample directions) is
+    # traced once with per-ray counters, and each block's node + triangle visits rank it (VERDICT r4 #3: the live-ray count ignores how long the live rays are).
     weights = (block_weights(big.rays, cfg["block"]).cpu().numpy()
                if (cfg["balance"] or cfg["order"]) and cfg["block"] > 0 else None)
     prio = weights if cfg["order"] else None
+    if cfg["order"] == 2 and cfg["block"] > 0:
+        other, _ = frame()
+        for a_, b_ in shard_launches(0, other.size, cfg["max_batch"]):
+            v = other.view(a_, b_)
+            # the per-lane order's counters: deterministic (the oracle's), so every rank derives the same deal
+            tracer.trace_batch(v, exact_rcp=exact, speculative=False, stats=True)
+            other.stats = v.stats if a_ == 0 else torch.cat([other.stats, v.stats])
+        prio = block_sums(other.stats[:, 0] + other.stats[:, 1], cfg["block"]).cpu().numpy()
+        del other
     deals = {}
 
     def owners_for(k):
@@ -1013,7 +1027,8 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
         "gathered_equals_single_gpu": equal, "streams": len(streams), "min_launches": cfg["min_launches"],
         "shards": (((f"{cfg['block']}-ray blocks dealt by live-ray count" if cfg["balance"]
                      else f"block-cyclic, {cfg['block']}-ray blocks")
-                    + (", live blocks first" if cfg["order"] else "")) if cfg["block"] > 0 else "contiguous"),
+                    + {0: "", 1: ", live blocks first", 2: ", costly blocks first (next frame's counters)"}[int(cfg["order"])])
+                   if cfg["block"] > 0 else "contiguous"),
         "projected_from_one_gpu": projected,
         "roofline": shard_roofline,
         "collective": f"{DIST_BACKEND} point-to-point gather of {n * 8} B to rank 0" if world > 1 else None,
@@ -1096,7 +1111,8 @@ def make_line(args, world, head, extras, strong, tracer_cfg):
                   "ray_type": "diffuse", "rcp": args.rcp,
                   "parallelism": ((f"one RayBuffer in {world} shards of {STRONG['block']}-ray blocks "
                                    + ("dealt by live-ray count" if STRONG["balance"] else "dealt round-robin (block-cyclic)")
-                                   + (", each shard's live blocks first" if STRONG["order"] else "")
+                                   + {0: "", 1: ", each shard's live blocks first",
+                                      2: ", each shard's costly blocks first (the next frame's counters)"}[int(STRONG["order"])]
                                    + ", BVH replicated, no collective in the step")
                                   if STRONG["block"] > 0 else f"one RayBuffer in {world} contiguous shards"),
                   "launch_rays_max": STRONG["max_batch"]}
@@ -1158,8 +1174,9 @@ def main():
                     help="block-cyclic shard block (rays); 0 = contiguous shards")
     ap.add_argument("--strong-balance", type=int, default=int(STRONG["balance"]), choices=[0, 1],
                     help="1: deal the shard blocks by live-ray count (mrt.dist.balance_blocks); 0: cyclically")
-    ap.add_argument("--strong-order", type=int, default=int(STRONG["order"]), choices=[0, 1],
-                    help="1: each shard's blocks in decreasing live-ray count (mrt.dist.shard_spans priority)")
+    ap.add_argument("--strong-order", type=int, default=int(STRONG["order"]), choices=[0, 1, 2],
+                    help="0: each shard's blocks in frame order; 1: in decreasing live-ray count; 2: in decreasing "
+                         "traversal cost, counted on the next frame of the same view (mrt.dist.shard_spans priority)")
     ap.add_argument("--strong-streams", type=int, default=STRONG["streams"], choices=[1, 2],
                     help="caller streams the strong-scaling launches alternate over")
     ap.add_argument("--strong-min-launches", type=int, default=STRONG["min_launches"],
@@ -1245,7 +1262,7 @@ def main():
         STRONG["block"] = max(0, args.strong_block)
         STRONG["streams"] = args.strong_streams
         STRONG["balance"] = bool(args.strong_balance)
-        STRONG["order"] = bool(args.strong_order)
+        STRONG["order"] = int(args.strong_order)
         STRONG["scene"] = args.strong_scene
         STRONG["w"], STRONG["h"], STRONG["spp"] = (int(v) for v in args.strong_size.split("x"))
         STRONG["name"] = f"{STRONG['scene']}-diffuse-{STRONG['w']}x{STRONG['h']}x{STRONG['spp']}spp"

@@ -44,6 +44,19 @@ def block_weights(rays: torch.Tensor, block: int) -> torch.Tensor:
     return live.view(-1, block).sum(1)
 
 
+def block_sums(values: torch.Tensor, block: int) -> torch.Tensor:
+    """Per-block sums of a per-ray value (e.g. a traced frame's node + triangle counts,
+    the STATS counters): the traversal cost of each block-ray block, a finer priority
+    for shard_spans than block_weights' live-ray count."""
+    if block <= 0:
+        raise ValueError("block_sums: block must be positive")
+    v = values.to(torch.int64).reshape(-1)
+    pad = (-v.numel()) % block
+    if pad:
+        v = torch.cat([v, v.new_zeros(pad)])
+    return v.view(-1, block).sum(1)
+
+
 def balance_blocks(weights, world: int) -> np.ndarray:
     """Owner rank of every block (int32 [nblocks]): the blocks in decreasing weight
     (ties: lower index first) dealt in serpentine order — ranks 0..world-1, then

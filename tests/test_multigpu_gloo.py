@@ -143,3 +143,16 @@ def test_two_ranks_on_one_gpu_trace_shards_and_gather(tmp_path):
     want, _, _ = O.trace(rays, *bufs, threads=8)
     assert len(got) == len(rays) == 173 * 91 * 3
     assert np.array_equal(got, want[:, :2])
+
+
+def test_block_sums_and_weights():
+    """Per-block traversal cost (mrt.dist.block_sums, the strong-scaling cost order) and the
+    live-ray count (block_weights): a ragged last block is summed over its rays only."""
+    from mrt.dist import block_sums, block_weights
+    v = torch.arange(10, dtype=torch.int32)
+    assert block_sums(v, 4).tolist() == [6, 22, 17]
+    rays = torch.zeros((10, 8))
+    rays[[0, 5, 9], 7] = -1.0
+    assert block_weights(rays, 4).tolist() == [3, 3, 1]
+    spans = shard_spans(10, 1, 0, 4, priority=block_sums(v, 4))
+    assert spans == [(4, 10), (0, 4)]   # costliest block first (adjacent blocks 1, 2 merged)
