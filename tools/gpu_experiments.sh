@@ -23,8 +23,9 @@
 #   ao_knobs     Mori / Fairy AO under launch knobs the autotuner does not explore
 #   timeline_shard  per-ray timeline of shard 0, live first vs frame order (variants/tailtl build)
 # Round-5 experiments:
-#   r5_guard     the unserved-queue sweep's cost: this tree vs the round-4 kernel (variants/r4, built at
-#                d775aa0 by tools/build_variant.sh r4 "" d775aa0) on the saved schedules  -> profiles/round5_guard_ab.txt
+#   r5_guard     the unserved-queue sweep's cost: variants/noroot (this tree without the LDS root) vs the
+#                round-4 kernel (variants/r4, tools/build_variant.sh r4 "" d775aa0), saved schedules
+#   r5_root      the root visit from LDS: lib vs variants/noroot (tools/build_variant.sh noroot -DMRT_ROOT_LDS=0)
 #   r5_hb640     hairball diffuse 640x480: global vs per-XCD queues x refill x waves x slack
 #   r5_ao        Mori / Fairy AO: grid size and the frontier tail
 # Usage: gpurun -- 'bash tools/gpu_experiments.sh order order2'
@@ -195,8 +196,14 @@ print('block $B balance $BAL T1', d['t1_ms'], 'one-stream', d.get('one_stream_ms
     r5_guard)
       timeout -k 10 600 python -u tools/ab.py --rounds 11 --launches 30 --workload hairball-diffuse-1920x1080 \
         --workload bunny-primary-1024x768 --workload hairball-diffuse-640x480 --workload conference-ao-640x480 \
-        --variant 'lib:{"saved":1}' --variant 'variants/r4:{"saved":1}' > $O/ab_guard.txt 2> $O/ab_guard.err || fail ab $O/ab_guard.err
+        --variant 'variants/noroot:{"saved":1}' --variant 'variants/r4:{"saved":1}' > $O/ab_guard.txt 2> $O/ab_guard.err || fail ab $O/ab_guard.err
       cat $O/ab_guard.txt ;;
+    r5_root)   # the root visit from LDS: this tree vs variants/noroot (-DMRT_ROOT_LDS=0), saved schedules
+      timeout -k 10 600 python -u tools/ab.py --rounds 9 --launches 30 --workload bunny-primary-1024x768 --workload bunny-primary-640x480 \
+        --workload conference-ao-640x480 --workload sponza-diffuse-640x480 --workload hairball-diffuse-640x480 \
+        --workload hairball-diffuse-1920x1080 --workload mori-ao-640x480 --workload fairy-ao-640x480 \
+        --variant 'lib:{"saved":1}' --variant 'variants/noroot:{"saved":1}' > $O/ab_root.txt 2> $O/ab_root.err || fail ab $O/ab_root.err
+      cat $O/ab_root.txt ;;
     r5_hb640)
       V='--variant lib:{"saved":1}'
       for W in 12 16; do for T in 40 48 56; do
