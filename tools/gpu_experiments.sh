@@ -28,6 +28,7 @@
 #   r5_root      the root visit from LDS: lib vs variants/noroot (tools/build_variant.sh noroot -DMRT_ROOT_LDS=0)
 #   r5_hb640     hairball diffuse 640x480: global vs per-XCD queues x refill x waves x slack
 #   r5_ao        Mori / Fairy AO: grid size and the frontier tail
+#   r5_order     projected eta(n) of the strong-scaling shards: live blocks first vs costly blocks first
 # Usage: gpurun -- 'bash tools/gpu_experiments.sh order order2'
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -225,6 +226,14 @@ print('block $B balance $BAL T1', d['t1_ms'], 'one-stream', d.get('one_stream_ms
       timeout -k 10 600 python -u tools/ab.py --rounds 7 --launches 30 --workload mori-ao-640x480 --workload fairy-ao-640x480 $V \
         > $O/ab_ao5.txt 2> $O/ab_ao5.err || fail ab $O/ab_ao5.err
       cat $O/ab_ao5.txt ;;
+    r5_order)   # projected eta(2/4/8) with the shard blocks live-first (1) vs cost-first (2), three runs each
+      for run in 1 2 3; do for OR in 1 2; do
+        timeout -k 10 400 python bench.py --no-extra --no-cpu --no-explore --no-fast --steps 5 --strong-order $OR \
+          --detail-out $O/order${OR}_$run.json > $O/order${OR}_$run.line 2> $O/order${OR}_$run.err || fail bench $O/order${OR}_$run.err
+        python3 -c "
+import json; d=json.load(open('$O/order${OR}_$run.json'))['strong']
+print('order $OR run $run T1', d['t1_ms'], {k: (v['eta'], max(v['shard_ms'])) for k, v in d['projected_from_one_gpu'].items()})" | tee -a $O/order_r5.txt
+      done; done ;;
     *) echo "unknown experiment $exp"; exit 2 ;;
   esac
 done
