@@ -197,13 +197,13 @@ print('block $B balance $BAL T1', d['t1_ms'], 'one-stream', d.get('one_stream_ms
     r5_guard)
       timeout -k 10 600 python -u tools/ab.py --rounds 11 --launches 30 --workload hairball-diffuse-1920x1080 \
         --workload bunny-primary-1024x768 --workload hairball-diffuse-640x480 --workload conference-ao-640x480 \
-        --variant 'variants/noroot:{"saved":1}' --variant 'variants/r4:{"saved":1}' > $O/ab_guard.txt 2> $O/ab_guard.err || fail ab $O/ab_guard.err
+        --variant 'lib/variants/noroot:{"saved":1}' --variant 'lib/variants/r4:{"saved":1}' > $O/ab_guard.txt 2> $O/ab_guard.err || fail ab $O/ab_guard.err
       cat $O/ab_guard.txt ;;
     r5_root)   # the root visit from LDS: this tree vs variants/noroot (-DMRT_ROOT_LDS=0), saved schedules
       timeout -k 10 600 python -u tools/ab.py --rounds 9 --launches 30 --workload bunny-primary-1024x768 --workload bunny-primary-640x480 \
         --workload conference-ao-640x480 --workload sponza-diffuse-640x480 --workload hairball-diffuse-640x480 \
         --workload hairball-diffuse-1920x1080 --workload mori-ao-640x480 --workload fairy-ao-640x480 \
-        --variant 'lib:{"saved":1}' --variant 'variants/noroot:{"saved":1}' > $O/ab_root.txt 2> $O/ab_root.err || fail ab $O/ab_root.err
+        --variant 'lib:{"saved":1}' --variant 'lib/variants/noroot:{"saved":1}' > $O/ab_root.txt 2> $O/ab_root.err || fail ab $O/ab_root.err
       cat $O/ab_root.txt ;;
     r5_hb640)
       V='--variant lib:{"saved":1}'
