@@ -22,9 +22,10 @@ constexpr int kQueueStrideWords = 64;      // one 256-B line per queue head
 #define MRT_BLOCK_THREADS 256
 #endif
 constexpr int kBlockThreads = MRT_BLOCK_THREADS;   // wave64s per workgroup x 64 (default 4 waves)
-// Queue heads: kMaxQueues per-XCD heads and the shared queue's head, one 256-B line each,
-// zeroed per launch.
-constexpr int kQueueLines = kMaxQueues + 1;
+// Queue heads: kMaxQueues per-XCD heads, the shared queue's head and the served mask (bit q:
+// some wave has taken from queue q), one 256-B line each, zeroed per launch.
+constexpr int kServedLine = kMaxQueues + 1;
+constexpr int kQueueLines = kMaxQueues + 2;
 // Largest node / woop buffer a tracer binds (32-bit buffer offsets).
 constexpr int64_t kMaxBufferBytes = 0xFFFFFFC0ll;
 
