@@ -219,7 +219,9 @@ def test_exact_reciprocal_is_correctly_rounded_for_every_float(tracer):
                                  dict(num_queues=8, queue_block=64, waves_per_cu=4),
                                  dict(num_queues=5, queue_shared=5, queue_block=1024, fetch_threshold=40, waves_per_cu=4),
                                  dict(num_queues=8, queue_block=8192, fetch_threshold=56, waves_per_cu=20),
-                                 dict(num_queues=8, queue_block=256, fetch_threshold=56, waves_per_cu=4)],
+                                 dict(num_queues=8, queue_block=256, fetch_threshold=56, waves_per_cu=4),
+                                 dict(ray_sort=1), dict(ray_sort=1, tail_lanes=0), dict(ray_sort=1, waves_per_cu=4),
+                                 dict(ray_sort=1, lane_groups=16), dict(ray_sort=1, waves_per_cu=8, lds_stack=8)],
                          ids=lambda c: ",".join(f"{k}={v}" for k, v in c.items()))
 def test_launch_configs_do_not_change_results(tracer, cfg):
     bufs, rays, any_hit, want, st = scene_setup("conference", 256, 192, "diffuse")
@@ -254,6 +256,28 @@ def test_queues_without_waves_are_still_traced(tracer, cfg):
         assert tracer.last_info["num_queues"] == cfg["num_queues"]
         res, gst = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=False, stats=True)
         assert np.array_equal(res[:, :2], want[:, :2]) and np.array_equal(gst[:, :3], st[:, :3])
+    finally:
+        tracer.set_config(**saved)
+
+
+@pytest.mark.parametrize("wl", [("conference", 640, 480, "ao"), ("mori", 640, 480, "ao"), ("sponza", 640, 480, "diffuse"),
+                                ("hairball:800", 640, 480, "diffuse"), ("bunny", 640, 480, "primary")],
+                         ids=lambda w: "-".join(map(str, w)))
+@pytest.mark.parametrize("waves", [20, 8])
+def test_ray_sort_traces_every_ray_once(tracer, wl, waves):
+    """cfg.ray_sort: a one-round static launch deals each workgroup's 256-ray tile by direction
+    octant (degenerate rays last). Every ray is traced exactly once and equals the oracle:
+    closest hits bit-identical, any hits genuine (hit/miss identical). At 8 waves/CU the
+    307 200-ray batch needs several rounds, so the sort is skipped there (the same results)."""
+    bufs, rays, any_hit, want, _ = scene_setup(*wl)
+    saved = tracer.config()
+    try:
+        tracer.set_config(ray_sort=1, waves_per_cu=waves, autotune=0)
+        res, _ = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=True)
+        if any_hit:
+            assert_valid_hits(rays, res, want, bufs)
+        else:
+            assert np.array_equal(res[:, :2], want[:, :2])
     finally:
         tracer.set_config(**saved)
 

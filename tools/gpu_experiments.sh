@@ -28,6 +28,7 @@
 #   r5_root      the root visit from LDS: lib vs variants/noroot (tools/build_variant.sh noroot -DMRT_ROOT_LDS=0)
 #   r5_hb640     hairball diffuse 640x480: global vs per-XCD queues x refill x waves x slack
 #   r5_ao        Mori / Fairy AO: grid size and the frontier tail
+#   r5_sort      the octant ray sort (cfg.ray_sort) of one-round static launches on the 307 k-ray batches
 #   r5_order     projected eta(n) of the strong-scaling shards: live blocks first vs costly blocks first
 # Usage: gpurun -- 'bash tools/gpu_experiments.sh order order2'
 set -o pipefail
@@ -234,6 +235,14 @@ print('block $B balance $BAL T1', d['t1_ms'], 'one-stream', d.get('one_stream_ms
 import json; d=json.load(open('$O/order${OR}_$run.json'))['strong']
 print('order $OR run $run T1', d['t1_ms'], {k: (v['eta'], max(v['shard_ms'])) for k, v in d['projected_from_one_gpu'].items()})" | tee -a $O/order_r5.txt
       done; done ;;
+    r5_sort)   # the octant ray sort of one-round static launches
+      V='--variant lib:{"saved":1} --variant lib:{"autotune":0} --variant lib:{"autotune":0,"ray_sort":1}'
+      V="$V --variant lib:{\"autotune\":0,\"ray_sort\":1,\"tail_lanes\":0} --variant lib:{\"autotune\":0,\"ray_sort\":1,\"spec_slack\":4}"
+      timeout -k 10 600 python -u tools/ab.py --rounds 7 --launches 30 --workload mori-ao-640x480 --workload fairy-ao-640x480 \
+        --workload conference-ao-640x480 --workload sponza-ao-640x480 --workload san-ao-640x480 --workload bunny-primary-640x480 \
+        --workload sponza-diffuse-640x480 --workload hairball-diffuse-640x480 --workload mori-diffuse-640x480 $V \
+        > $O/ab_sort.txt 2> $O/ab_sort.err || fail ab $O/ab_sort.err
+      cat $O/ab_sort.txt ;;
     *) echo "unknown experiment $exp"; exit 2 ;;
   esac
 done
