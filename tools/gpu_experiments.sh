@@ -247,7 +247,7 @@ print('order $OR run $run T1', d['t1_ms'], {k: (v['eta'], max(v['shard_ms'])) fo
       timeout -k 10 600 python -u tools/ab.py --rounds 9 --launches 30 --workload hairball-diffuse-640x480 \
         --workload hairball-diffuse-1920x1080 --workload bunny-primary-1024x768 --workload bunny-primary-640x480 \
         --workload conference-ao-640x480 --workload sponza-diffuse-640x480 --workload mori-ao-640x480 \
-        --variant 'lib:{"saved":1}' --variant 'lib/variants/presort:{"saved":1}' --variant 'lib/variants/r4:{"saved":1}' \
+        --variant 'lib:{"saved":1}' --variant 'lib/variants/presort:{"saved":1}' --variant 'lib/variants/sort0:{"saved":1}' \
         > $O/ab_regs.txt 2> $O/ab_regs.err || fail ab $O/ab_regs.err
       cat $O/ab_regs.txt ;;
     *) echo "unknown experiment $exp"; exit 2 ;;
