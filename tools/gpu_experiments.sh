@@ -250,6 +250,12 @@ print('order $OR run $run T1', d['t1_ms'], {k: (v['eta'], max(v['shard_ms'])) fo
         --variant 'lib:{"saved":1}' --variant 'lib/variants/presort:{"saved":1}' --variant 'lib/variants/sort0:{"saved":1}' \
         > $O/ab_regs.txt 2> $O/ab_regs.err || fail ab $O/ab_regs.err
       cat $O/ab_regs.txt ;;
+    r5_probe)   # which part of the (disabled) ray-sort block speeds the kernel up: its LDS, or a barrier
+      timeout -k 10 600 python -u tools/ab.py --rounds 9 --launches 30 --workload hairball-diffuse-1920x1080 \
+        --workload bunny-primary-1024x768 --workload sponza-diffuse-640x480 --workload hairball-diffuse-640x480 \
+        --variant 'lib:{"saved":1}' --variant 'lib/variants/sort0:{"saved":1}' --variant 'lib/variants/ldspad:{"saved":1}' \
+        --variant 'lib/variants/dbar:{"saved":1}' > $O/ab_probe.txt 2> $O/ab_probe.err || fail ab $O/ab_probe.err
+      cat $O/ab_probe.txt ;;
     *) echo "unknown experiment $exp"; exit 2 ;;
   esac
 done
