@@ -256,6 +256,13 @@ print('order $OR run $run T1', d['t1_ms'], {k: (v['eta'], max(v['shard_ms'])) fo
         --variant 'lib:{"saved":1}' --variant 'lib/variants/sort0:{"saved":1}' --variant 'lib/variants/ldspad:{"saved":1}' \
         --variant 'lib/variants/dbar:{"saved":1}' > $O/ab_probe.txt 2> $O/ab_probe.err || fail ab $O/ab_probe.err
       cat $O/ab_probe.txt ;;
+    r5_nops)   # is the dead-code speed-up code placement? sort0 shifted by 1/2/4/8 s_nop
+      timeout -k 10 600 python -u tools/ab.py --rounds 9 --launches 30 --workload hairball-diffuse-640x480 \
+        --workload bunny-primary-1024x768 --workload hairball-diffuse-1920x1080 \
+        --variant 'lib:{"saved":1}' --variant 'lib/variants/sort0:{"saved":1}' --variant 'lib/variants/nop1:{"saved":1}' \
+        --variant 'lib/variants/nop2:{"saved":1}' --variant 'lib/variants/nop4:{"saved":1}' --variant 'lib/variants/nop8:{"saved":1}' \
+        > $O/ab_nops.txt 2> $O/ab_nops.err || fail ab $O/ab_nops.err
+      cat $O/ab_nops.txt ;;
     *) echo "unknown experiment $exp"; exit 2 ;;
   esac
 done
