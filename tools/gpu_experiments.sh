@@ -261,6 +261,7 @@ print('order $OR run $run T1', d['t1_ms'], {k: (v['eta'], max(v['shard_ms'])) fo
         --workload bunny-primary-1024x768 --workload hairball-diffuse-1920x1080 \
         --variant 'lib:{"saved":1}' --variant 'lib/variants/sort0:{"saved":1}' --variant 'lib/variants/nop1:{"saved":1}' \
         --variant 'lib/variants/nop2:{"saved":1}' --variant 'lib/variants/nop4:{"saved":1}' --variant 'lib/variants/nop8:{"saved":1}' \
+        --variant 'lib/variants/al64:{"saved":1}' --variant 'lib/variants/cur_al64:{"saved":1}' \
         > $O/ab_nops.txt 2> $O/ab_nops.err || fail ab $O/ab_nops.err
       cat $O/ab_nops.txt ;;
     *) echo "unknown experiment $exp"; exit 2 ;;
