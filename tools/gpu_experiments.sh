@@ -264,6 +264,12 @@ print('order $OR run $run T1', d['t1_ms'], {k: (v['eta'], max(v['shard_ms'])) fo
         --variant 'lib/variants/al64:{"saved":1}' --variant 'lib/variants/cur_al64:{"saved":1}' \
         > $O/ab_nops.txt 2> $O/ab_nops.err || fail ab $O/ab_nops.err
       cat $O/ab_nops.txt ;;
+    r5_slack)   # any-hit batches: turn to the postponed leaves earlier (spec_slack 8 .. 63 = as soon as one lane has one)
+      V='--variant lib:{"autotune":0}'
+      for K in 8 16 32 48 63; do V="$V --variant lib:{\"autotune\":0,\"spec_slack\":$K}"; done
+      timeout -k 10 600 python -u tools/ab.py --rounds 7 --launches 30 --workload mori-ao-640x480 --workload fairy-ao-640x480 \
+        --workload conference-ao-640x480 --workload sponza-ao-640x480 $V > $O/ab_slack.txt 2> $O/ab_slack.err || fail ab $O/ab_slack.err
+      cat $O/ab_slack.txt ;;
     *) echo "unknown experiment $exp"; exit 2 ;;
   esac
 done
