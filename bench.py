@@ -923,13 +923,16 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
     # timed steps — a rank generating its own rays would produce them in shard order —
     # but it is timed here (max over ranks), so the line can say what a Renderer that
     # shards an existing buffer pays on top: value_with_gather_and_shard.
+    def build_local():
+        if world == 1:   # T_1's buffer: the whole frame, in the same block order as the shards when they are ordered
+            return shard_buffer(1, 0) if prio is not None else big
+        return shard_buffer(world, rank)
+
+    local = build_local()   # (the first build also pays PyTorch's one-time kernel setup: timed on a second one)
     torch.cuda.synchronize()
     barrier(world)
     ts = time.perf_counter()
-    if world == 1:   # T_1's buffer: the whole frame, in the same block order as the shards when they are ordered
-        local = shard_buffer(1, 0) if prio is not None else big
-    else:
-        local = shard_buffer(world, rank)
+    local = build_local()
     torch.cuda.synchronize()
     shard_build_ms = reduce_over_ranks(1e3 * (time.perf_counter() - ts), world)
     # The shard's <= 2^21-ray launches are independent batches: they alternate
