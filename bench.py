@@ -60,7 +60,7 @@ L2_PEAK_GBS = 34500.0    # the eight XCD L2s together (§L2)
 LINE_BYTES = 128         # gfx950 L1 and L2 line: one TCP_TCC_READ_REQ / TCC_EA0_RDREQ per line
                          # (tools/ubench_levels.hip, profiles/round3_counter_calibration.md)
 MALL_BYTES = 256 << 20   # Infinity Cache: a BVH above this streams from HBM
-PROFILE_TAGS = ("round4",)   # committed rocprofv3 summaries the line may cite, newest first
+PROFILE_TAGS = ("round5", "round4")   # committed rocprofv3 summaries the line may cite, newest first
                                       # (profiles/<tag>_<workload>_*): only one of the timed schedule is cited
 PROFILE_RATIO = (0.9, 1.1)   # a cited profile's mean kernel time / this run's event time must lie in here
 LATENCY_BOUND = 0.25         # every memory level served below this fraction of its ceiling: bound = "latency"
