@@ -270,6 +270,17 @@ print('order $OR run $run T1', d['t1_ms'], {k: (v['eta'], max(v['shard_ms'])) fo
       timeout -k 10 600 python -u tools/ab.py --rounds 7 --launches 30 --workload mori-ao-640x480 --workload fairy-ao-640x480 \
         --workload conference-ao-640x480 --workload sponza-ao-640x480 $V > $O/ab_slack.txt 2> $O/ab_slack.err || fail ab $O/ab_slack.err
       cat $O/ab_slack.txt ;;
+    r5_steal)   # end-of-batch queue stealing (cfg.queue_steal): its code's cost (off, vs variants/presteal) and its effect
+      X='"autotune":0,"num_queues":8,"fetch_threshold":56,"waves_per_cu":20,"spec_slack":6,"queue_block":8192'
+      Y='"autotune":0,"num_queues":8,"fetch_threshold":48,"waves_per_cu":12'
+      timeout -k 10 600 python -u tools/ab.py --rounds 9 --launches 30 --workload hairball-diffuse-1920x1080 \
+        --workload hairball-diffuse-640x480 --workload bunny-primary-1024x768 --workload sponza-diffuse-640x480 \
+        --variant 'lib:{"saved":1}' --variant 'lib/variants/presteal:{"saved":1}' \
+        --variant "lib:{$X}" --variant "lib:{$X,\"queue_steal\":1}" \
+        --variant "lib:{$Y,\"queue_block\":1024}" --variant "lib:{$Y,\"queue_block\":1024,\"queue_steal\":1}" \
+        --variant "lib:{$Y,\"queue_block\":4096,\"queue_steal\":1}" \
+        > $O/ab_steal.txt 2> $O/ab_steal.err || fail ab $O/ab_steal.err
+      cat $O/ab_steal.txt ;;
     *) echo "unknown experiment $exp"; exit 2 ;;
   esac
 done
