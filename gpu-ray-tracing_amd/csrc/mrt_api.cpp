@@ -220,7 +220,6 @@ mrt_launch_cfg default_cfg() {
     c.tail_lanes = kDefaultTailLanes;
     c.queue_shared = 0;
     c.queue_block = 0;
-    c.queue_steal = 0;
     c.ray_sort = 0;
     c.queue_xcc_mask = 0;
     return c;
@@ -236,8 +235,7 @@ bool valid_cfg(const mrt_launch_cfg& c) {
            c.tail_lanes >= 0 && c.tail_lanes <= 16 &&
            c.queue_shared >= 0 && c.queue_shared <= 100 && c.queue_block >= 0 && c.queue_block <= (1 << 20) &&
            (c.queue_block & (c.queue_block - 1)) == 0 && (c.queue_block == 0 || c.queue_block >= 64) &&
-           c.queue_xcc_mask >= 0 && c.queue_xcc_mask <= 15 && (c.ray_sort == 0 || c.ray_sort == 1) &&
-           (c.queue_steal == 0 || c.queue_steal == 1);
+           c.queue_xcc_mask >= 0 && c.queue_xcc_mask <= 15 && (c.ray_sort == 0 || c.ray_sort == 1);
 }
 
 // The frontier tail runs in the exact 4-wide kernels whose leaf refs carry counts.
@@ -717,7 +715,6 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     a.tailLanes = cfg.tail_lanes;
     a.xccMask = cfg.queue_xcc_mask;
     a.raySort = cfg.ray_sort;
-    a.queueSteal = cfg.queue_steal;
     a.queues = ws->queues;
     a.spill = ws->spill;
     // The blocking call counts this launch's overflows in a slot of its own; the
@@ -933,7 +930,6 @@ int mrt_tracer_set_config(mrt_tracer* t, const mrt_launch_cfg* cfg) {
     if (c.queue_block < 0) c.queue_block = d.queue_block;
     if (c.queue_xcc_mask < 0) c.queue_xcc_mask = d.queue_xcc_mask;
     if (c.ray_sort < 0) c.ray_sort = d.ray_sort;
-    if (c.queue_steal < 0) c.queue_steal = d.queue_steal;
     if (!valid_cfg(c)) return fail(MRT_ERR_INVALID_ARG, "launch config out of range");
     std::lock_guard<std::mutex> lock(t->mu);
     t->cfg = c;

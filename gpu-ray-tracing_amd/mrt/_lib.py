@@ -34,7 +34,7 @@ vp, i32, i64, u32, f32 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_float
 class LaunchCfg(C.Structure):
     _fields_ = [("waves_per_cu", i32), ("fetch_threshold", i32), ("num_queues", i32), ("lds_stack", i32),
                 ("lane_groups", i32), ("wide", i32), ("spec_slack", i32), ("static_rounds", i32), ("autotune", i32),
-                ("tail_lanes", i32), ("queue_shared", i32), ("queue_block", i32), ("queue_steal", i32), ("ray_sort", i32),
+                ("tail_lanes", i32), ("queue_shared", i32), ("queue_block", i32), ("ray_sort", i32),
                 ("queue_xcc_mask", i32)]
 
 

@@ -129,9 +129,6 @@ typedef struct mrt_launch_cfg {
                                   the shares are this many rays' blocks dealt cyclically (block i to queue
                                   i mod num_queues), so every XCD samples the whole frame (default 0;
                                   -1 = default)                                                        */
-    int32_t queue_steal;       /* num_queues > 1, frontier-tail kernels: 1 = a wave whose own queue (and the shared
-                                  and any unserved one) is dry helps the queue with the most rays left (more
-                                  than 512) instead of stopping; 0 = off (default; -1 = default)           */
     int32_t ray_sort;          /* 1 = a static launch whose batch fits one round of the grid (e.g. 307 200 rays
                                   at 20 waves/CU) deals each workgroup's 256 consecutive rays to its four
                                   waves by direction octant, degenerate (tmax < 0) rays last, instead of
