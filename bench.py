@@ -23,7 +23,8 @@ replicated). Two scalings are measured in every run:
     fixed RayBuffer — hairball diffuse 1920x1080 x 8 spp = 16.6 M rays, generated
     as the reference's Renderer does in <= 2^21-ray batches (Renderer.cc:46,
     RayGen.cc:124-142) — cut into block-cyclic shards (1 024-ray blocks dealt
-    round-robin to the ranks; --strong-balance 1 deals them by live-ray count),
+    round-robin to the ranks; --strong-balance 1 deals them by live-ray count, 2 by the
+    next frame's traversal cost),
     each shard's blocks ordered live rays first (--strong-order; T_1's buffer
     too), each traced in <= 2^21-ray launches with no collective; T_n = max over
     ranks. T_1 is measured in the same run (rank 0
@@ -112,7 +113,7 @@ EXTRA_N1 = ["bunny-primary-640x480", "conference-ao-640x480", "sponza-diffuse-64
 # Strong-scaling config: scene, frame, samples per pixel, rays per launch.
 # min_launches: a shard is cut into at least this many launches (alternating over two streams).
 STRONG = {"name": "hairball-diffuse-1920x1080x8spp", "scene": "hairball", "w": 1920, "h": 1080, "spp": 8,
-          "max_batch": 1 << 21, "min_launches": 1, "block": 1 << 10, "streams": 2, "balance": False,
+          "max_batch": 1 << 21, "min_launches": 1, "block": 1 << 10, "streams": 2, "balance": 0,
           "order": 1}
 STRONG_PROJECT = (2, 4, 8)   # N=1 only: rank counts whose per-rank shards are timed on the one GPU
 
@@ -892,25 +893,27 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
     # Order 2's cost is what a renderer knows from the frame before: the NEXT frame of the
     # same view (the following rand() seeds: the same pixels, other sample directions) is
     # traced once with per-ray counters, and each block's node + triangle visits rank it (the live-ray count ignores how long the live rays are).
+    # Balance 2 deals the blocks by that cost instead of the live-ray count (equal work per rank).
     weights = (block_weights(big.rays, cfg["block"]).cpu().numpy()
                if (cfg["balance"] or cfg["order"]) and cfg["block"] > 0 else None)
-    prio = weights if cfg["order"] else None
-    if cfg["order"] == 2 and cfg["block"] > 0:
+    cost = None
+    if (cfg["order"] == 2 or cfg["balance"] == 2) and cfg["block"] > 0:
         other, _ = frame()
         for a_, b_ in shard_launches(0, other.size, cfg["max_batch"]):
             v = other.view(a_, b_)
             # the per-lane order's counters: deterministic (the oracle's), so every rank derives the same deal
             tracer.trace_batch(v, exact_rcp=exact, speculative=False, stats=True)
             other.stats = v.stats if a_ == 0 else torch.cat([other.stats, v.stats])
-        prio = block_sums(other.stats[:, 0] + other.stats[:, 1], cfg["block"]).cpu().numpy()
+        cost = block_sums(other.stats[:, 0] + other.stats[:, 1], cfg["block"]).cpu().numpy()
         del other
+    prio = {0: None, 1: weights, 2: cost}[int(cfg["order"])]
     deals = {}
 
     def owners_for(k):
         if weights is None or k == 1 or not cfg["balance"]:
             return None
         if k not in deals:
-            deals[k] = balance_blocks(weights, k)
+            deals[k] = balance_blocks(cost if cfg["balance"] == 2 else weights, k)
         return deals[k]
 
     def shard_buffer(k, rk):
@@ -1028,7 +1031,8 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
         "schedule": {str(k): v for k, v in scheds.items()},
         "schedule_name": "; ".join(sorted({v["name"] for v in scheds.values()})),
         "gathered_equals_single_gpu": equal, "streams": len(streams), "min_launches": cfg["min_launches"],
-        "shards": (((f"{cfg['block']}-ray blocks dealt by live-ray count" if cfg["balance"]
+        "shards": (((f"{cfg['block']}-ray blocks dealt by " + ("the next frame's cost" if cfg["balance"] == 2
+                                                                else "live-ray count") if cfg["balance"]
                      else f"block-cyclic, {cfg['block']}-ray blocks")
                     + {0: "", 1: ", live blocks first", 2: ", costly blocks first (next frame's counters)"}[int(cfg["order"])])
                    if cfg["block"] > 0 else "contiguous"),
@@ -1113,7 +1117,8 @@ def make_line(args, world, head, extras, strong, tracer_cfg):
                   "rays_counted": strong["rays_counted"],
                   "ray_type": "diffuse", "rcp": args.rcp,
                   "parallelism": ((f"one RayBuffer in {world} shards of {STRONG['block']}-ray blocks "
-                                   + ("dealt by live-ray count" if STRONG["balance"] else "dealt round-robin (block-cyclic)")
+                                   + ({1: "dealt by live-ray count", 2: "dealt by the next frame's traversal cost"}.get(
+                                       int(STRONG["balance"]), "dealt round-robin (block-cyclic)"))
                                    + {0: "", 1: ", each shard's live blocks first",
                                       2: ", each shard's costly blocks first (the next frame's counters)"}[int(STRONG["order"])]
                                    + ", BVH replicated, no collective in the step")
@@ -1175,8 +1180,9 @@ def main():
     ap.add_argument("--strong-steps", type=int, default=50)
     ap.add_argument("--strong-block", type=int, default=STRONG["block"],
                     help="block-cyclic shard block (rays); 0 = contiguous shards")
-    ap.add_argument("--strong-balance", type=int, default=int(STRONG["balance"]), choices=[0, 1],
-                    help="1: deal the shard blocks by live-ray count (mrt.dist.balance_blocks); 0: cyclically")
+    ap.add_argument("--strong-balance", type=int, default=int(STRONG["balance"]), choices=[0, 1, 2],
+                    help="0: deal the shard blocks cyclically; 1: by live-ray count, 2: by the next frame's traversal "
+                         "cost (mrt.dist.balance_blocks: equal weight per rank)")
     ap.add_argument("--strong-order", type=int, default=int(STRONG["order"]), choices=[0, 1, 2],
                     help="0: each shard's blocks in frame order; 1: in decreasing live-ray count; 2: in decreasing "
                          "traversal cost, counted on the next frame of the same view (mrt.dist.shard_spans priority)")
@@ -1264,7 +1270,7 @@ def main():
         STRONG["min_launches"] = max(1, args.strong_min_launches)
         STRONG["block"] = max(0, args.strong_block)
         STRONG["streams"] = args.strong_streams
-        STRONG["balance"] = bool(args.strong_balance)
+        STRONG["balance"] = int(args.strong_balance)
         STRONG["order"] = int(args.strong_order)
         STRONG["scene"] = args.strong_scene
         STRONG["w"], STRONG["h"], STRONG["spp"] = (int(v) for v in args.strong_size.split("x"))

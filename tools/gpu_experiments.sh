@@ -281,6 +281,14 @@ print('order $OR run $run T1', d['t1_ms'], {k: (v['eta'], max(v['shard_ms'])) fo
         --variant "lib:{$Y,\"queue_block\":4096,\"queue_steal\":1}" \
         > $O/ab_steal.txt 2> $O/ab_steal.err || fail ab $O/ab_steal.err
       cat $O/ab_steal.txt ;;
+    r5_balance)   # projected eta(n): blocks dealt cyclically (0) vs by the next frame's cost (2), live-first order, three runs each
+      for run in 1 2 3; do for BAL in 0 2; do
+        timeout -k 10 400 python bench.py --no-extra --no-cpu --no-explore --no-fast --steps 5 --strong-balance $BAL \
+          --detail-out $O/bal${BAL}_$run.json > $O/bal${BAL}_$run.line 2> $O/bal${BAL}_$run.err || fail bench $O/bal${BAL}_$run.err
+        python3 -c "
+import json; d=json.load(open('$O/bal${BAL}_$run.json'))['strong']
+print('balance $BAL run $run T1', d['t1_ms'], {k: (v['eta'], max(v['shard_ms']), min(v['shard_ms'])) for k, v in d['projected_from_one_gpu'].items()})" | tee -a $O/balance_r5.txt
+      done; done ;;
     *) echo "unknown experiment $exp"; exit 2 ;;
   esac
 done
