@@ -289,6 +289,15 @@ print('order $OR run $run T1', d['t1_ms'], {k: (v['eta'], max(v['shard_ms'])) fo
 import json; d=json.load(open('$O/bal${BAL}_$run.json'))['strong']
 print('balance $BAL run $run T1', d['t1_ms'], {k: (v['eta'], max(v['shard_ms']), min(v['shard_ms'])) for k, v in d['projected_from_one_gpu'].items()})" | tee -a $O/balance_r5.txt
       done; done ;;
+    r5_head)   # the headline batch around its saved schedule (static rounds, 8 waves/CU, 2 lane groups, slack 6)
+      V='--variant lib:{"saved":1}'
+      for c in '"spec_slack":8' '"spec_slack":10' '"tail_lanes":8' '"tail_lanes":0' '"lds_stack":8' '"lane_groups":4' \
+               '"waves_per_cu":12' '"waves_per_cu":4' '"lane_groups":2,"spec_slack":4' '"static_rounds":1,"spec_slack":7'; do
+        V="$V --variant lib:{\"autotune\":0,\"waves_per_cu\":8,\"lane_groups\":2,\"spec_slack\":6,$c}"
+      done
+      timeout -k 10 600 python -u tools/ab.py --rounds 9 --launches 30 --workload bunny-primary-1024x768 $V \
+        > $O/ab_head5.txt 2> $O/ab_head5.err || fail ab $O/ab_head5.err
+      cat $O/ab_head5.txt ;;
     *) echo "unknown experiment $exp"; exit 2 ;;
   esac
 done
