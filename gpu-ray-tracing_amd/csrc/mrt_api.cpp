@@ -68,7 +68,7 @@ struct mrt_tracer {
 
     // Occupancy per kernel variant (index variant_key(), below 256), queried once
     // (hipOccupancy* is a host round-trip that would otherwise sit on every launch).
-    int occ[1024] = {};   // variant_key; | 512: the packet kernel of that variant
+    int occ[512] = {};
 
     // cfg.autotune: per (batch size, variant) the ray-distribution schedule the
     // measured launches chose (mrt_api.cpp autotune_*), reset on bind/set_config.
@@ -222,7 +222,6 @@ mrt_launch_cfg default_cfg() {
     c.queue_block = 0;
     c.ray_sort = 0;
     c.queue_xcc_mask = 0;
-    c.packet = 0;
     return c;
 }
 
@@ -236,8 +235,7 @@ bool valid_cfg(const mrt_launch_cfg& c) {
            c.tail_lanes >= 0 && c.tail_lanes <= 16 &&
            c.queue_shared >= 0 && c.queue_shared <= 100 && c.queue_block >= 0 && c.queue_block <= (1 << 20) &&
            (c.queue_block & (c.queue_block - 1)) == 0 && (c.queue_block == 0 || c.queue_block >= 64) &&
-           c.queue_xcc_mask >= 0 && c.queue_xcc_mask <= 15 && (c.ray_sort == 0 || c.ray_sort == 1) &&
-           (c.packet == 0 || c.packet == 1);
+           c.queue_xcc_mask >= 0 && c.queue_xcc_mask <= 15 && (c.ray_sort == 0 || c.ray_sort == 1);
 }
 
 // The frontier tail runs in the exact 4-wide kernels whose leaf refs carry counts.
@@ -340,23 +338,6 @@ int grid_blocks(mrt_tracer* t, const mrt_launch_cfg& cfg, const mrt::TraceVarian
     const int want = std::max(1, (waves + wavesPerBlock - 1) / wavesPerBlock);
     const int perCU = std::min(want, occ);
     if (outBlocksPerCU) *outBlocksPerCU = perCU;
-    return perCU * t->numCUs;
-}
-
-// The wave-packet traversal (cfg.packet) serves closest-hit launches over the exact 4-wide
-// nodes whose leaf refs carry counts and whose depth-first stack fits its wave stack.
-bool packet_fits(const mrt_tracer* t, const mrt::TraceVariant& v) {
-    return !v.anyHit && v.speculative && !v.stats && v.nodes == mrt::kNodeWide4 && t->wideLeafCounts &&
-           t->wideStackBound < mrt::kPacketStack;
-}
-
-// Its grid: waves_per_cu (0 = kPacketWaves) per CU, as many as its occupancy admits.
-constexpr int kPacketWaves = 16;
-int packet_blocks(mrt_tracer* t, const mrt_launch_cfg& cfg, const mrt::TraceVariant& v) {
-    int& occ = t->occ[variant_key(v) | 512];
-    if (occ <= 0 && (mrt::packet_occupancy(v.exactRcp, &occ) != hipSuccess || occ <= 0)) occ = 1;
-    const int waves = cfg.waves_per_cu ? cfg.waves_per_cu : kPacketWaves;
-    const int perCU = std::min(std::max(1, (waves + mrt::kBlockThreads / 64 - 1) / (mrt::kBlockThreads / 64)), occ);
     return perCU * t->numCUs;
 }
 
@@ -701,8 +682,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
         cfg = tune_candidate(t, cfg, cand, tune->stage1);
     }
     v.tail = with_tail(t, v, cfg);   // a tuned candidate may run without the tail
-    const bool packet = cfg.packet == 1 && packet_fits(t, v);
-    const int blocks = packet ? packet_blocks(t, cfg, v) : grid_blocks(t, cfg, v, numRays, &perCU);
+    const int blocks = grid_blocks(t, cfg, v, numRays, &perCU);
     const int totalLanes = blocks * mrt::kBlockThreads;
     const bool wide = v.nodes != mrt::kNodeCompact2;
     const int stackCap = wide ? t->wideStackCap : mrt::kStackCapacity;
@@ -744,15 +724,12 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
 
     hipStream_t s = static_cast<hipStream_t>(stream);
     // Queue heads restart at zero for every launch; strided mode has none.
-    if (a.numQueues > 0 || packet)
+    if (a.numQueues > 0)
         MRT_HIP(hipMemsetAsync(ws->queues, 0, mrt::kQueueLines * mrt::kQueueStrideWords * sizeof(unsigned), s));
     if (info) MRT_HIP(hipMemsetAsync(ws->status + mrt::kTimedSlot, 0, sizeof(int), s));
     if (info) MRT_HIP(hipEventRecord(t->evStart, s));
     if (slot) MRT_HIP(hipEventRecord(slot->start, s));
-    if (packet)
-        MRT_HIP(mrt::launch_packet(v.exactRcp, a, blocks, s));
-    else
-        MRT_HIP(mrt::launch_trace(v, a, blocks, s));
+    MRT_HIP(mrt::launch_trace(v, a, blocks, s));
 #ifdef MRT_DONE_EVENT
     MRT_HIP(hipEventRecord(ws->done, s));
 #endif
@@ -776,7 +753,6 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
         info->node_bytes = v.nodes == mrt::kNodeWide4 ? 128 : 64;
         info->num_queues = a.numQueues;
         info->fetch_threshold = a.fetchThreshold;
-        info->packet = packet ? 1 : 0;
         int overflow = 0;
         MRT_HIP(hipMemcpy(&overflow, ws->status + mrt::kTimedSlot, sizeof(int), hipMemcpyDeviceToHost));
         info->stack_overflows = overflow;
@@ -954,7 +930,6 @@ int mrt_tracer_set_config(mrt_tracer* t, const mrt_launch_cfg* cfg) {
     if (c.queue_block < 0) c.queue_block = d.queue_block;
     if (c.queue_xcc_mask < 0) c.queue_xcc_mask = d.queue_xcc_mask;
     if (c.ray_sort < 0) c.ray_sort = d.ray_sort;
-    if (c.packet < 0) c.packet = d.packet;
     if (!valid_cfg(c)) return fail(MRT_ERR_INVALID_ARG, "launch config out of range");
     std::lock_guard<std::mutex> lock(t->mu);
     t->cfg = c;

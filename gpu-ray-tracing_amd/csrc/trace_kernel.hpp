@@ -109,13 +109,6 @@ hipError_t trace_occupancy(const TraceVariant& v, int* blocksPerCU);
 // Static facts about a variant's code object (for occupancy sizing/reporting).
 hipError_t trace_kernel_attributes(const TraceVariant& v, hipFuncAttributes* attr);
 
-// The wave-packet traversal (packet_kernel.hip): closest hit over exact 4-wide nodes whose
-// leaf refs carry counts, 64-ray tiles per wave; a.queues[g] (zeroed) is XCD group g's tile
-// head. Its wave stack holds kPacketStack entries: the caller checks stackBound against it.
-constexpr int kPacketStack = 64;
-hipError_t launch_packet(bool exactRcp, const TraceArgs& a, int gridBlocks, hipStream_t s);
-hipError_t packet_occupancy(bool exactRcp, int* blocksPerCU);
-
 // Exhaustive check of the EXACT variants' reciprocal against 1.0f / x (all 2^32
 // inputs); adds the number of mismatching bit patterns to *mismatchesDev.
 hipError_t selftest_exact_rcp(unsigned long long* mismatchesDev, hipStream_t s);

@@ -35,13 +35,13 @@ class LaunchCfg(C.Structure):
     _fields_ = [("waves_per_cu", i32), ("fetch_threshold", i32), ("num_queues", i32), ("lds_stack", i32),
                 ("lane_groups", i32), ("wide", i32), ("spec_slack", i32), ("static_rounds", i32), ("autotune", i32),
                 ("tail_lanes", i32), ("queue_shared", i32), ("queue_block", i32), ("ray_sort", i32),
-                ("queue_xcc_mask", i32), ("packet", i32)]
+                ("queue_xcc_mask", i32)]
 
 
 class TraceInfo(C.Structure):
     _fields_ = [("kernel_ms", f32), ("grid_waves", i32), ("block_threads", i32),
                 ("lds_stack_entries", i32), ("wide", i32), ("num_queues", i32), ("fetch_threshold", i32), ("stack_overflows", i32), ("node_bytes", i32),
-                ("autotune_candidate", i32), ("autotune_locked", i32), ("stack_capacity", i32), ("packet", i32)]
+                ("autotune_candidate", i32), ("autotune_locked", i32), ("stack_capacity", i32)]
 
 
 class BindInfo(C.Structure):

@@ -137,12 +137,6 @@ typedef struct mrt_launch_cfg {
     int32_t queue_xcc_mask;    /* test hook, 0 = off (default; -1 = default): 1..15 = a wave takes from queue
                                   (XCC_ID & mask) % num_queues, so with mask 3 and 8 queues, queues 4..7
                                   have no waves of their own (the unserved-queue sweep must trace them) */
-    int32_t packet;            /* 1 = closest-hit launches over the exact 4-wide nodes (leaf refs with counts,
-                                  wave stack bound below 64 entries) use the wave-packet traversal: each
-                                  wave walks the tree once for its 64-ray tile, node and triangle rows in
-                                  scalar registers, each child entered by the lanes that hit its box
-                                  (closest hits unchanged except exact-t ties); waves_per_cu sizes its
-                                  grid (0 = 16). Other launches ignore it. 0 = off (default; -1 = default) */
 } mrt_launch_cfg;
 
 /* Per-launch statistics reported back to the host (optional). */
@@ -167,7 +161,6 @@ typedef struct mrt_trace_info {
     int32_t stack_capacity;    /* stack entries (sentinel included) the launch had: 64 = the reference's
                                   for the binary order; the wide orders get the bound tree's worst case
                                   (never less than 64), so no ray of a tree overflows there          */
-    int32_t packet;            /* 1 when the launch ran the wave-packet traversal (cfg.packet)       */
 } mrt_trace_info;
 
 /* What the last bind derived (mrt_tracer_bind_info). */

@@ -282,33 +282,6 @@ def test_ray_sort_traces_every_ray_once(tracer, wl, waves):
         tracer.set_config(**saved)
 
 
-@pytest.mark.parametrize("wl", [("bunny", 640, 480, "primary"), ("conference", 640, 480, "primary"),
-                                ("sponza", 640, 480, "diffuse"), ("mori", 256, 192, "diffuse"),
-                                ("conference", 256, 192, "ao"), ("bunny", 97, 61, "primary")],
-                         ids=lambda w: "-".join(map(str, w)))
-@pytest.mark.parametrize("waves", [16, 4])
-def test_packet_traversal_matches_oracle(tracer, wl, waves):
-    """cfg.packet: closest-hit launches walk the tree once per 64-ray tile (packet_kernel.hip),
-    each lane testing only what its own walk reaches; closest hits bit-identical to the oracle
-    in both reciprocal modes' exact form, every ray traced once (a ragged last tile of the
-    97x61 batch included, 4 waves/CU: several tiles per wave through the XCD group heads).
-    Any-hit launches ignore the knob (launch info packet 0) and stay genuine."""
-    bufs, rays, any_hit, want, _ = scene_setup(*wl)
-    saved = tracer.config()
-    try:
-        tracer.set_config(packet=1, waves_per_cu=waves, autotune=0)
-        res, _ = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=True)
-        if any_hit:
-            assert tracer.last_info["packet"] == 0
-            assert_valid_hits(rays, res, want, bufs)
-        else:
-            assert tracer.last_info["packet"] == 1
-            assert np.array_equal(res[:, :2], want[:, :2])
-            assert tracer.last_info["stack_overflows"] == 0
-    finally:
-        tracer.set_config(**saved)
-
-
 def test_per_xcd_candidate_uses_one_queue_per_xcd(tracer):
     """The autotuner's per-XCD candidate (2) sizes its queues from the device's XCD count
     (hipDeviceAttributeNumberOfXccs), never more: 8 on an SPX MI355X."""
