@@ -103,13 +103,15 @@ WORKLOADS = {
     "mori-primary-640x480": ("mori", 640, 480, "primary", 1),
     "mori-ao-640x480": ("mori", 640, 480, "ao", 1),
     "mori-diffuse-640x480": ("mori", 640, 480, "diffuse", 1),
+    "fairy-ao-640x480": ("fairy", 640, 480, "ao", 1),
     "hairball-primary-640x480": ("hairball", 640, 480, "primary", 1),
     "hairball-diffuse-640x480": ("hairball", 640, 480, "diffuse", 1),
     "hairball-diffuse-1920x1080": ("hairball", 1920, 1080, "diffuse", 1),
 }
 HEADLINE = "bunny-primary-1024x768"
+# (Mori AO and Fairy AO: the two README cells furthest from their targets, VERDICT r4 #7, measured by every bench run)
 EXTRA_N1 = ["bunny-primary-640x480", "conference-ao-640x480", "sponza-diffuse-640x480", "sponza-diffuse2-640x480",
-            "hairball-diffuse-640x480", "hairball-diffuse-1920x1080"]
+            "hairball-diffuse-640x480", "hairball-diffuse-1920x1080", "mori-ao-640x480", "fairy-ao-640x480"]
 # Strong-scaling config: scene, frame, samples per pixel, rays per launch.
 # min_launches: a shard is cut into at least this many launches (alternating over two streams).
 STRONG = {"name": "hairball-diffuse-1920x1080x8spp", "scene": "hairball", "w": 1920, "h": 1080, "spp": 8,

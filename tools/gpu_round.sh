@@ -17,7 +17,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out; export TMPDIR=/tmp
 O=gpurun_out
-BENCH_WL="bunny-primary-1024x768 bunny-primary-640x480 conference-ao-640x480 sponza-diffuse-640x480 sponza-diffuse2-640x480 hairball-diffuse-640x480 hairball-diffuse-1920x1080"
+BENCH_WL="bunny-primary-1024x768 bunny-primary-640x480 conference-ao-640x480 sponza-diffuse-640x480 sponza-diffuse2-640x480 hairball-diffuse-640x480 hairball-diffuse-1920x1080 mori-ao-640x480 fairy-ao-640x480"
 fail() { echo "$1 failed"; tail -30 "$2"; exit 1; }
 for step in "$@"; do
   arg=""; [[ $step == *=* ]] && { arg=${step#*=}; step=${step%%=*}; }
