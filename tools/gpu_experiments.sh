@@ -30,6 +30,8 @@
 #   r5_ao        Mori / Fairy AO: grid size and the frontier tail
 #   r5_sort      the octant ray sort (cfg.ray_sort) of one-round static launches on the 307 k-ray batches
 #   r5_order     projected eta(n) of the strong-scaling shards: live blocks first vs costly blocks first
+#   (later round-5 A/Bs — the packet traversal, top levels in LDS, scheduler flags, XCD shares, ray prefetch —
+#    were run from throwaway scripts against tools/build_variant.sh builds; their outputs are profiles/round5_*_ab.txt)
 # Usage: gpurun -- 'bash tools/gpu_experiments.sh order order2'
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -271,6 +273,7 @@ print('order $OR run $run T1', d['t1_ms'], {k: (v['eta'], max(v['shard_ms'])) fo
         --workload conference-ao-640x480 --workload sponza-ao-640x480 $V > $O/ab_slack.txt 2> $O/ab_slack.err || fail ab $O/ab_slack.err
       cat $O/ab_slack.txt ;;
     r5_steal)   # end-of-batch queue stealing (cfg.queue_steal): its code's cost (off, vs variants/presteal) and its effect
+                # (the knob was removed after this run: check out aff58af to repeat it)
       X='"autotune":0,"num_queues":8,"fetch_threshold":56,"waves_per_cu":20,"spec_slack":6,"queue_block":8192'
       Y='"autotune":0,"num_queues":8,"fetch_threshold":48,"waves_per_cu":12'
       timeout -k 10 600 python -u tools/ab.py --rounds 9 --launches 30 --workload hairball-diffuse-1920x1080 \
