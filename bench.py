@@ -10,7 +10,7 @@ HBM. The headline workload (BASELINE.json configs[1]) is Bunny primary rays at
 stand-ins with the published triangle counts (the OBJ assets are absent).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME] [--extra/--no-extra]
-                  [--scaling weak|strong]
+                  [--readme-cells default|all|none] [--scaling weak|strong]
 
 Multi-GPU (one rank per GPU, RCCL): under torch.distributed.run (WORLD_SIZE set)
 every process is one rank; `python bench.py --gpus N` without a launcher starts
@@ -36,8 +36,9 @@ replicated). Two scalings are measured in every run:
     Halton (2,3) point in each pixel).
 
 Rank 0 prints one JSON line (kept under 10 kB: the headline, its roofline and CPU
-baseline, strong scaling and a few numbers per extra workload); the full per-workload
-detail goes to --detail-out.
+baseline, strong scaling, a few numbers per extra workload and, at N = 1, the other
+README cells with their ratio to the README and the oracle's agreement); the full
+per-workload detail goes to --detail-out.
 """
 from __future__ import annotations
 
@@ -104,6 +105,12 @@ WORKLOADS = {
     "mori-ao-640x480": ("mori", 640, 480, "ao", 1),
     "mori-diffuse-640x480": ("mori", 640, 480, "diffuse", 1),
     "fairy-ao-640x480": ("fairy", 640, 480, "ao", 1),
+    "fairy-diffuse-640x480": ("fairy", 640, 480, "diffuse", 1),
+    "dragon-primary-640x480": ("dragon", 640, 480, "primary", 1),
+    "sibenik-diffuse-640x480": ("sibenik", 640, 480, "diffuse", 1),
+    "sibenik-ao-640x480": ("sibenik", 640, 480, "ao", 1),
+    "san-diffuse-640x480": ("san", 640, 480, "diffuse", 1),
+    "san-ao-640x480": ("san", 640, 480, "ao", 1),
     "hairball-primary-640x480": ("hairball", 640, 480, "primary", 1),
     "hairball-diffuse-640x480": ("hairball", 640, 480, "diffuse", 1),
     "hairball-diffuse-1920x1080": ("hairball", 1920, 1080, "diffuse", 1),
@@ -112,6 +119,14 @@ HEADLINE = "bunny-primary-1024x768"
 # (Mori AO and Fairy AO: the two README cells furthest from their targets, VERDICT r4 #7, measured by every bench run)
 EXTRA_N1 = ["bunny-primary-640x480", "conference-ao-640x480", "sponza-diffuse-640x480", "sponza-diffuse2-640x480",
             "hairball-diffuse-640x480", "hairball-diffuse-1920x1080", "mori-ao-640x480", "fairy-ao-640x480"]
+# The other README cells (README.md:61-81) a default N = 1 run measures too, so that the driver's own run checks
+# them (14 of 17 cells were measured only by tools/readme_table.py): timed steps with the schedule
+# saved for the BVH or settled by the autotuner in the warmup, and the oracle's agreement. San Miguel's two
+# cells (a 10.5 M-triangle SBVH build on the host) only with --readme-cells all.
+README_N1 = ["sponza-primary-640x480", "sponza-ao-640x480", "mori-primary-640x480", "mori-diffuse-640x480",
+             "hairball-primary-640x480", "dragon-primary-640x480", "conference-diffuse-640x480",
+             "fairy-diffuse-640x480", "sibenik-diffuse-640x480", "sibenik-ao-640x480"]
+README_ALL = README_N1 + ["san-diffuse-640x480", "san-ao-640x480"]
 # Strong-scaling config: scene, frame, samples per pixel, rays per launch.
 # min_launches: a shard is cut into at least this many launches (alternating over two streams).
 STRONG = {"name": "hairball-diffuse-1920x1080x8spp", "scene": "hairball", "w": 1920, "h": 1080, "spp": 8,
@@ -778,6 +793,27 @@ def schedule_of(tracer, rb, exact):
             "fetch_threshold": li["fetch_threshold"], "grid_waves": li["grid_waves"]}
 
 
+def readme_cell(name, tracer, scenes, steps, warmup, exact, want_cpu):
+    """One README cell at N = 1 (README_N1): the workload's batches timed like a bench step,
+    its schedule, and — in the cpu_baseline leg — the oracle's agreement on every ray."""
+    scene_name = workload_spec(name)[0]
+    e = scenes.get(scene_name)
+    batches = Batches(name, e["scene"], e["gbvh"], tracer, 0)
+    launches = [tracer.launcher(rb, exact_rcp=exact) for rb, _ in batches.batches]
+    wall, launch_ms, _ = time_steps(launches, steps, warmup, 1)
+    value = batches.rays_counted * steps / wall / 1e6
+    sched = schedule_of(tracer, batches.batches[0][0], exact)
+    ref = REFERENCE_MRAYS[name]
+    out = {"cell": name, "value": round(value, 1), "x_readme": round(value / ref, 2), "kernel_ms": round(launch_ms, 4),
+           "schedule": sched["name"], "saved": bool(batches.locked_from_store)}
+    if want_cpu:
+        cb = cpu_baseline(batches.batches, scenes.host_buffers(scene_name), batches.rays_counted, host_threads(),
+                          name)
+        out["agree"] = cb["parity_exact_fraction"]   # any hit: hit/miss identical and every differing hit valid
+        out["cpu"] = cb["value"]
+    return out
+
+
 def run_workload(name, tracer, scenes, world, rank, steps, warmup, exact, want_cpu, explore=False, fast=False):
     scene_name = workload_spec(name)[0]
     e = scenes.get(scene_name)
@@ -1110,7 +1146,7 @@ def compact_strong(st):
     return keep
 
 
-def make_line(args, world, head, extras, strong, tracer_cfg):
+def make_line(args, world, head, extras, strong, tracer_cfg, cells=None):
     """(the one stdout line, the full detail). The line stays under LINE_MAX_BYTES
     (tests/test_bench_line.py builds it from a recorded run)."""
     ref = REFERENCE_MRAYS.get(args.workload)
@@ -1161,10 +1197,13 @@ def make_line(args, world, head, extras, strong, tracer_cfg):
                       "roofline": compact_roofline(head["rcp_fast"]["roofline"])} if head.get("rcp_fast") else None),
         "autotune_exploration": head.get("autotune_exploration"),
         "extra_workloads": [compact_workload(r) for r in extras],
+        "readme_cells": ([{k: c[k] for k in ("cell", "value", "x_readme", "agree") if k in c} for c in cells]
+                         if cells else None),
     }
     if strong is not None and args.scaling == "strong" and strong.get("gathered_equals_single_gpu") is False:
         line["error"] = "gathered results differ from the single-GPU results"
-    detail = {"args": vars(args), "tracer_config": tracer_cfg, "head": head, "extras": extras, "strong": strong}
+    detail = {"args": vars(args), "tracer_config": tracer_cfg, "head": head, "extras": extras, "strong": strong,
+              "readme_cells": cells}
     return line, detail
 
 
@@ -1184,6 +1223,9 @@ def main():
     ap.add_argument("--extra", dest="extra", action="store_true", default=None,
                     help="also measure the AO/diffuse/hairball configs (default on at N=1)")
     ap.add_argument("--no-extra", dest="extra", action="store_false")
+    ap.add_argument("--readme-cells", choices=("default", "all", "none"), default="default",
+                    help="with the extras (N = 1): the other README cells, README_N1 (default), all 17 incl. "
+                         "San Miguel (a 10.5 M-triangle SBVH build), or none")
     ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling measurement")
     ap.add_argument("--strong-steps", type=int, default=50)
     ap.add_argument("--strong-block", type=int, default=STRONG["block"],
@@ -1273,6 +1315,12 @@ def main():
                 extras.append(r)
                 log(f"[extra] {name}: {r['value']} Mrays/s (reference {r['reference_mrays']}, "
                     f"cpu {r.get('cpu_baseline', {}).get('value')})")
+    cells = []
+    readme = {"default": README_N1, "all": README_ALL, "none": []}[args.readme_cells] if do_extra else []
+    for name in readme:
+        c = readme_cell(name, tracer, scenes, min(args.steps, 50), args.warmup, exact, want_cpu)
+        cells.append(c)
+        log(f"[readme] {name}: {c['value']} Mrays/s ({c['x_readme']}x README, agree {c.get('agree')})")
     strong = None
     if not args.no_strong or args.scaling == "strong":
         STRONG["min_launches"] = max(1, args.strong_min_launches)
@@ -1290,7 +1338,7 @@ def main():
             f"{ {k: v['eta'] for k, v in (strong['projected_from_one_gpu'] or {}).items()} }")
 
     if rank == 0:
-        line, detail = make_line(args, world, head, extras, strong, tracer.config())
+        line, detail = make_line(args, world, head, extras, strong, tracer.config(), cells)
         if args.detail_out:
             os.makedirs(os.path.dirname(os.path.abspath(args.detail_out)), exist_ok=True)
             with open(args.detail_out, "w") as f:

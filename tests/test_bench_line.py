@@ -34,19 +34,20 @@ def round3_detail():
 
 
 def details():
-    out = [("round3", *round3_detail())]
-    path = os.path.join(REPO, "profiles", "round4_bench_detail.json")
-    if os.path.exists(path):
-        with open(path) as f:
-            d = json.load(f)
-        out.append(("round4", d["head"], d["extras"], d["strong"]))
+    out = [("round3", *round3_detail(), None)]
+    for tag in ("round4", "round5"):
+        path = os.path.join(REPO, "profiles", f"{tag}_bench_detail.json")
+        if os.path.exists(path):
+            with open(path) as f:
+                d = json.load(f)
+            out.append((tag, d["head"], d["extras"], d["strong"], d.get("readme_cells")))
     return out
 
 
 @pytest.mark.parametrize("rec", details(), ids=lambda r: r[0])
 def test_line_is_small_and_complete_at_n1(rec):
-    _, head, extras, strong = rec
-    line, detail = bench.make_line(args_for("weak"), 1, head, extras, strong, {})
+    _, head, extras, strong, cells = rec
+    line, detail = bench.make_line(args_for("weak"), 1, head, extras, strong, {}, cells)
     text = json.dumps(line, separators=(",", ":"))
     assert len(text) < 10_000 and len(text) <= bench.LINE_MAX_BYTES
     assert "\n" not in text and json.loads(text) == line
@@ -70,7 +71,7 @@ def test_line_is_small_and_complete_at_n1(rec):
 def test_line_at_n_gt_1_is_the_strong_scaling_number(rec):
     """at N > 1 the value is the sharded hairball RayBuffer (BASELINE configs[4]),
     ms_per_step its T_n, the parallelism names block-cyclic shards; weak scaling is a sub-block."""
-    _, head, _, strong = rec
+    _, head, _, strong, _ = rec
     st = dict(strong, n_gpus=2, tn_ms=strong["t1_ms"] / 1.9, eta=0.95)
     st["value"] = round(st["rays_counted"] / (st["tn_ms"] * 1e-3) / 1e6, 2)
     line, _ = bench.make_line(args_for("strong"), 2, head, [], st, {})
@@ -80,3 +81,24 @@ def test_line_at_n_gt_1_is_the_strong_scaling_number(rec):
     assert line["weak_scaling"]["value"] == head["value"]
     assert line["strong_scaling"]["value_n1_same_run"] > 0
     assert len(json.dumps(line)) < 10_000
+
+
+def test_readme_cells_ride_on_the_n1_line():
+    """The README cells of a default N = 1 run (bench.README_N1) are on the line, each with its ratio to the
+    README and the oracle agreement, and the line with all of them still fits (round 5's recorded run)."""
+    path = os.path.join(REPO, "profiles", "round5_bench_detail.json")
+    if not os.path.exists(path):
+        pytest.skip("no round-5 detail file")
+    with open(path) as f:
+        d = json.load(f)
+    cells = d.get("readme_cells")
+    if not cells:
+        pytest.skip("recorded run without README cells")
+    line, _ = bench.make_line(args_for("weak"), 1, d["head"], d["extras"], d["strong"], {}, cells)
+    text = json.dumps(line, separators=(",", ":"))
+    assert len(text) <= bench.LINE_MAX_BYTES
+    got = {c["cell"] for c in line["readme_cells"]}
+    assert got == set(bench.README_N1)
+    for c in line["readme_cells"]:
+        assert c["x_readme"] > 1 and c["agree"] == 1.0
+        assert abs(c["value"] / bench.REFERENCE_MRAYS[c["cell"]] - c["x_readme"]) < 0.01
