@@ -265,8 +265,11 @@ def launch_ranks(n, argv, script=None, poll_s=0.2, grace_s=30.0):
             time.sleep(poll_s)
         for p in procs:
             p.wait()
-        if rc == 0:
-            rc = next((p.returncode for p in procs if p.returncode != 0), 0)
+        if rc == 0:   # every rank ended within one poll: report the first failure here
+            failed = [r for r, p in enumerate(procs) if p.returncode != 0]
+            if failed:
+                rc = procs[failed[0]].returncode
+                log(f"[launch] rank {failed[0]} exited with {rc}" + (f" (ranks {failed} failed)" if len(failed) > 1 else ""))
     finally:
         for s, h in old.items():
             signal.signal(s, h)
@@ -625,7 +628,7 @@ def cpu_baseline(batches, bufs, counted, threads, label, fast_results=None):
     import oracle_lib as O
     nodes, woop, tri = bufs
     host = [(rb.rays.cpu().numpy(), not rb.need_closest_hit, rb.results_numpy()) for rb, _ in batches]
-    secs, agree, n, any_checked = [], 0, 0, 0
+    secs, agree, n, any_checked, ties = [], 0, 0, 0, 0
     fast = {"rays": 0, "mismatch": 0, "tie": 0, "edge": 0, "other": 0, "any_hit_outcome_flips": 0,
             "any_hit_invalid": 0} if fast_results is not None else None
     for rep in range(6):
@@ -641,6 +644,9 @@ def cpu_baseline(batches, bufs, counted, threads, label, fast_results=None):
                     same = (gpu[:, 0] == -1) == (res[:, 0] == -1)
                     same[bad] = False
                     any_checked += len(diff)
+                else:   # another triangle at exactly the oracle's t: a tie the traversal order breaks
+                    t_eq = np.nonzero(~same & (gpu[:, 1] == res[:, 1]))[0]
+                    ties += len(t_eq) - len(O.invalid_hits(rays, gpu, woop, tri, which=t_eq))
                 agree += int(same.sum())
                 n += len(rays)
                 if fast is not None:
@@ -665,8 +671,8 @@ def cpu_baseline(batches, bufs, counted, threads, label, fast_results=None):
            "cpu_model": cpu_model(), "seconds_best": round(best, 4),
            "sample": f"{label}: all {len(host)} batch(es), {rays} rays ({counted} counted), best of 5 after 1 "
                      f"warmup, {threads} threads, oracle/trace_oracle.c (same Compact2 bytes, same rays)",
-           "parity_exact_fraction": round(agree / max(1, n), 6),
-           "any_hit_valid_hits_checked": any_checked}
+           "parity_exact_fraction": round(agree / max(1, n), 6), "parity_rays": n, "parity_same": agree,
+           "closest_hit_exact_t_ties": ties, "any_hit_valid_hits_checked": any_checked}
     if fast is not None:
         fast["tie_fraction"] = round(fast["tie"] / max(1, fast["rays"]), 8)
         out["rcp_fast_parity"] = fast
@@ -810,6 +816,8 @@ def readme_cell(name, tracer, scenes, steps, warmup, exact, want_cpu):
         cb = cpu_baseline(batches.batches, scenes.host_buffers(scene_name), batches.rays_counted, host_threads(),
                           name)
         out["agree"] = cb["parity_exact_fraction"]   # any hit: hit/miss identical and every differing hit valid
+        if cb["closest_hit_exact_t_ties"]:
+            out["ties"] = cb["closest_hit_exact_t_ties"]
         out["cpu"] = cb["value"]
     return out
 
@@ -1108,6 +1116,8 @@ def compact_parity(cb, fast):
     out = {"exact_fraction": cb.get("parity_exact_fraction")} if cb else {}
     if cb and cb.get("any_hit_valid_hits_checked"):
         out["any_hit_valid_hits_checked"] = cb["any_hit_valid_hits_checked"]
+    if cb and cb.get("closest_hit_exact_t_ties"):
+        out["closest_hit_exact_t_ties"] = cb["closest_hit_exact_t_ties"]
     if fast and fast.get("parity"):
         fp = fast["parity"]
         out["rcp_fast"] = {k: fp[k] for k in ("rays", "mismatch", "tie", "edge", "other", "any_hit_outcome_flips",
@@ -1197,7 +1207,7 @@ def make_line(args, world, head, extras, strong, tracer_cfg, cells=None):
                       "roofline": compact_roofline(head["rcp_fast"]["roofline"])} if head.get("rcp_fast") else None),
         "autotune_exploration": head.get("autotune_exploration"),
         "extra_workloads": [compact_workload(r) for r in extras],
-        "readme_cells": ([{k: c[k] for k in ("cell", "value", "x_readme", "agree") if k in c} for c in cells]
+        "readme_cells": ([{k: c[k] for k in ("cell", "value", "x_readme", "agree", "ties") if k in c} for c in cells]
                          if cells else None),
     }
     if strong is not None and args.scaling == "strong" and strong.get("gathered_equals_single_gpu") is False:

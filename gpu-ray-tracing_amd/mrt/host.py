@@ -63,6 +63,8 @@ class Scene:
     def __init__(self, handle: int, name: str):
         self._h = C.c_void_p(handle)
         self.name = name
+        # bound now: at interpreter exit the module's globals may already be gone when __del__ runs
+        self._destroy = _lib.host_lib().mrth_scene_destroy
 
     @classmethod
     def synthetic(cls, name: str, param: int = 0, seed: int = 1) -> "Scene":
@@ -86,7 +88,7 @@ class Scene:
 
     def __del__(self):
         if getattr(self, "_h", None) and self._h.value:
-            _lib.host_lib().mrth_scene_destroy(self._h)
+            self._destroy(self._h)
             self._h = C.c_void_p()
 
     @property
@@ -134,6 +136,7 @@ class Bvh:
 
     def __init__(self, handle: int):
         self._h = C.c_void_p(handle)
+        self._destroy = _lib.host_lib().mrth_bvh_destroy   # bound now, as in Scene
 
     @classmethod
     def build(cls, scene: Scene, max_leaf: int = 8, min_leaf: int = 1, split_alpha: float = 1e-5,
@@ -196,7 +199,7 @@ class Bvh:
 
     def __del__(self):
         if getattr(self, "_h", None) and self._h.value:
-            _lib.host_lib().mrth_bvh_destroy(self._h)
+            self._destroy(self._h)
             self._h = C.c_void_p()
 
     def buffers(self):

@@ -89,7 +89,7 @@ def main():
         value = batches.rays_counted * args.steps / wall / 1e6
         kernel_ms = launch_ms * len(batches.batches)
         # Parity of every ray of every batch (the timed launches' results) against the oracle.
-        n, same, checked = 0, 0, 0
+        n, same, checked, ties = 0, 0, 0, 0
         for rb, _ in batches.batches:
             k = rb.size if args.parity_rays <= 0 else min(args.parity_rays, rb.size)
             rays = rb.rays.cpu().numpy()[:k]
@@ -103,7 +103,12 @@ def main():
                 same += int(ok.sum())
                 checked += len(diff)
             else:
-                same += int(((gpu[:, 0] == ref[:, 0]) & (gpu[:, 1] == ref[:, 1])).sum())
+                eq = (gpu[:, 0] == ref[:, 0]) & (gpu[:, 1] == ref[:, 1])
+                same += int(eq.sum())
+                # another triangle at exactly the oracle's t (coincident surfaces): which one wins follows
+                # the traversal order; counted apart, each re-verified as a Woop hit at that t
+                t_eq = np.nonzero(~eq & (gpu[:, 1] == ref[:, 1]))[0]
+                ties += len(t_eq) - len(O.invalid_hits(rays, gpu, bufs[1], bufs[2], which=t_eq))
             n += k
         agree = same / max(1, n)
         row = {
@@ -117,6 +122,7 @@ def main():
             "schedule": bench.schedule_of(tracer, batches.batches[0][0], True)["name"],
             "parity_rays": n, "parity_all_rays": n == batches.rays_traced, "parity_agree": agree, "parity_kind": "valid hits" if any_hit else "id+t exact",
             "any_hit_results_reverified": checked if any_hit else None,
+            "parity_same": same, "exact_t_ties": None if any_hit else ties,
         }
         rows.append(row)
         print(json.dumps(row), flush=True)
@@ -137,6 +143,24 @@ README_INNER_NODES = {"bunny": 50876, "dragon": 301376, "conference": 105025, "h
                       "mori": 3483}
 
 
+def agreement(r):
+    """The oracle column: counts, not a rounded fraction (5 ties in 307 200 rays read 1.0000)."""
+    n = r["parity_rays"]
+    if r.get("parity_same") is None:   # a row of an older run
+        return f"{r['parity_agree']:.6f} ({r['parity_kind']}, {n} rays)"
+    same = r["parity_same"]
+    if r["parity_kind"] == "valid hits":
+        return f"{same}/{n} valid hits ({r['any_hit_results_reverified']} differing hits re-verified)"
+    ties = r.get("exact_t_ties") or 0
+    other = n - same - ties
+    text = f"{same}/{n} id+t exact"
+    if ties:
+        text += f", {ties} exact-t ties (another triangle at the oracle's t, a valid hit)"
+    if other:
+        text += f", **{other} other**"
+    return text
+
+
 def write_md(rows, out):
     # alg. GB/s: SURVEY §8(d)'s bytes per ray (cache hits included) over the kernel time; a rate, not a level's
     # traffic, so it may exceed the HBM peak (bench.py's roofline prices the per-level PMC bytes instead)
@@ -148,8 +172,7 @@ def write_md(rows, out):
         nodes = f"{r['inner_nodes']:,} / {ref:,}" if ref else f"{r['inner_nodes']:,} / —"
         md.append(f"| {r['workload']} (README:{r['readme_line']}) | {r['tris']:,} | {nodes} | {r['readme_mrays']} | "
                   f"**{r['mrays']}** | {r['x_readme']} | {r['kernel_ms']} | {r['per_ray']['nodes']} | "
-                  f"{r['per_ray']['tris']} | {r['alg_gbs']} | {r.get('schedule', '')} | {r['parity_agree']:.4f} ({r['parity_kind']}, "
-                  f"{r['parity_rays']} rays) |")
+                  f"{r['per_ray']['tris']} | {r['alg_gbs']} | {r.get('schedule', '')} | {agreement(r)} |")
     with open(os.path.join(out, "readme_table.md"), "w") as f:
         f.write("\n".join(md) + "\n")
     print("\n".join(md))
