@@ -58,8 +58,9 @@ for step in "$@"; do
       cp gpu-ray-tracing_amd/mrt/tuned_schedules.json $O/tuned_schedules_all.json
       W=$(python3 -c "import sys; sys.path.insert(0,'tools'); import readme_table as r; print(' '.join('--workload '+c[0] for c in r.CELLS))")
       timeout -k 10 900 python -u tools/tune_db.py $W --rounds 2 --launches 10 --out $O/tuned_schedules_all.json \
-        > $O/tune_db_readme.txt 2> $O/tune_db_readme.err || fail "tune readme" $O/tune_db_readme.err
-      timeout -k 10 900 python -u tools/readme_table.py --tune-db $O/tuned_schedules_all.json > $O/readme_table.log 2>&1 \
+        --out-cells $O/tuned_cells.json > $O/tune_db_readme.txt 2> $O/tune_db_readme.err || fail "tune readme" $O/tune_db_readme.err
+      timeout -k 10 900 python -u tools/readme_table.py --tune-db $O/tuned_schedules_all.json --cell-db $O/tuned_cells.json \
+        > $O/readme_table.log 2>&1 \
         || fail "readme table" $O/readme_table.log
       cat $O/readme_table.md ;;
     pipe)

@@ -55,7 +55,12 @@ def main():
     ap.add_argument("--parity-rays", type=int, default=0, help="rays per batch checked against the oracle (0 = all)")
     ap.add_argument("--cells", default="", help="comma-separated subset of workloads")
     ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out"))
-    ap.add_argument("--tune-db", default=None, help="saved schedules to lock (default: the package's)")
+    ap.add_argument("--cell-db", default=None,
+                    help="tools/tune_db.py --out-cells file: each cell locks its own tuned schedule (after the BVH's "
+                         "saved ones), so two ray types of one BVH and batch size each run their own")
+    ap.add_argument("--tune-db", default=None,
+                    help="saved schedules to lock (default: the package's; 'none': every cell's batch size is tuned "
+                         "live in its warmup, so two ray types of one BVH and batch size never share a schedule)")
     args = ap.parse_args()
 
     import numpy as np
@@ -67,7 +72,15 @@ def main():
     from mrt.schedules import DEFAULT_PATH, ScheduleStore
     torch.cuda.set_device(0)
     tracer = Tracer(0)
-    bench.STORE = ScheduleStore(args.tune_db or DEFAULT_PATH)   # cells without saved schedules autotune in warmup
+    # cells without a saved schedule for their BVH and batch size autotune in the warmup
+    bench.STORE = None if args.tune_db == "none" else ScheduleStore(args.tune_db or DEFAULT_PATH)
+    cell_db = {}
+    if args.cell_db:
+        with open(args.cell_db) as f:
+            cdb = json.load(f)
+        from mrt import _lib
+        if cdb.get("version") == _lib.MRT_TUNE_VERSION:
+            cell_db = cdb["cells"]
     want = set(args.cells.split(",")) if args.cells else None
     state = {"cell": "start", "t0": time.perf_counter()}
     stop = threading.Event()
@@ -83,6 +96,10 @@ def main():
         scene, build_s = e["scene"], e["build_s"]
         bufs = scenes.host_buffers(scene_name)
         batches = bench.Batches(name, scene, e["gbvh"], tracer)
+        own = cell_db.get(name)
+        if own and own["fingerprint"] == e["gbvh"].fingerprint:   # this cell's own tuned schedule
+            from mrt import _lib
+            tracer.load_schedules([(n, v, own["candidate"], _lib.MRT_TUNE_VERSION) for n, v in own["keys"]])
         alg_bytes, n_nodes, n_tris, n_leaves = bench.algorithmic_bytes(tracer, batches.batches)
         launches = [tracer.launcher(rb, exact_rcp=True) for rb, _ in batches.batches]
         wall, launch_ms, _ = bench.time_steps(launches, args.steps, args.warmup, 1)

@@ -39,6 +39,9 @@ def main():
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--fast-rcp", action="store_true", help="tune the v_rcp_f32 variant too")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--out-cells", default=None,
+                    help="also write each workload's own choice (JSON: workload -> keys, candidate): two ray types of "
+                         "one BVH and batch size share a key in --out, the last tuned wins there")
     ap.add_argument("--margin", type=float, default=MARGIN,
                     help="how much faster (median) a candidate must be to replace the rule (the library's 3 %%)")
     args = ap.parse_args()
@@ -55,6 +58,7 @@ def main():
     scenes = bench.SceneCache(1, 0, os.path.join(os.environ.get("TMPDIR", "/tmp"), "mrt_bvhcache"))
     wls = args.workload or [bench.HEADLINE] + bench.EXTRA_N1
     bench.STORE = None
+    cells = {}
     for wl in wls:
         e = scenes.get(bench.workload_spec(wl)[0])
         b = bench.Batches(wl, e["scene"], e["gbvh"], tracer)
@@ -114,12 +118,19 @@ def main():
             chosen = best2 if s2[best2] < (1 - args.margin) * s2[rule_c] else rule_c
             lock(chosen)
             store.update(e["gbvh"].fingerprint, tracer.schedules())
+            cells[f"{wl}{'' if exact else ':fast'}"] = {"fingerprint": e["gbvh"].fingerprint,
+                                                       "keys": [list(k) for k in keys], "candidate": chosen}
             print(f"{wl} exact={exact}: rule {rule_c} {s1[rule_c]:.4f} ms; sweep "
                   + " ".join(f"{c & 0xff}/{c >> 8}:{v:.4f}" for c, v in sorted(s1.items(), key=lambda kv: kv[1])[:6])
                   + "; final " + " ".join(f"{c & 0xff}/{c >> 8}:{v:.4f}" for c, v in s2.items())
                   + f" -> {chosen & 0xff}/{chosen >> 8} ({bench.schedule_name(chosen)})", flush=True)
     store.save(out)
     print(f"wrote {out}")
+    if args.out_cells:
+        import json
+        with open(args.out_cells, "w") as f:
+            json.dump({"version": _lib.MRT_TUNE_VERSION, "cells": cells}, f, indent=1)
+        print(f"wrote {args.out_cells}")
 
 
 if __name__ == "__main__":
