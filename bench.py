@@ -927,7 +927,8 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
         r.set_params(RAY_DIFFUSE, cfg["spp"])
         r.begin_frame(cam, cfg["w"], cfg["h"])
         parts = [b for b, _ in r.batches()]
-        return RayBuffer(torch.cat([b.rays for b in parts]), need_closest_hit=True), r.total_num_rays()
+        return (RayBuffer(torch.cat([b.rays for b in parts]), need_closest_hit=True, secondary=True),
+                r.total_num_rays())
 
     big, counted = frame()
     n = big.size
@@ -966,7 +967,7 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
         # the shard as one contiguous RayBuffer (built before the timed region: a
         # rank generating its own rays would produce it in this order directly)
         return RayBuffer(local_rays(big.rays, shard_spans(n, k, rk, cfg["block"], owners_for(k), prio)),
-                         need_closest_hit=True)
+                         need_closest_hit=True, secondary=True)
 
     # Building the shard's buffer (one index_select of its blocks) stays outside the
     # timed steps — a rank generating its own rays would produce them in shard order —

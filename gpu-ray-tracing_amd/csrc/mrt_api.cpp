@@ -275,6 +275,7 @@ constexpr int kAutoMinWaves = 8;
 // Persistent grid: as many 256-thread workgroups per CU as the config asks for
 // (or the batch size suggests) and the code object's occupancy admits; every
 // workgroup is resident at once.
+constexpr int kSecondaryKey = 512;   // tuning keys only: variant_key | kSecondaryKey for MRT_TRACE_SECONDARY batches
 int variant_key(const mrt::TraceVariant& v) {
     const int lds = v.ldsStack == 8 ? 0 : v.ldsStack == 16 ? 1 : 2;
     static_assert((15 | (2 << 4) | (mrt::kNodeWide4Q << 6) | (1 << 8)) < (int)(sizeof(mrt_tracer::occ) / sizeof(int)),
@@ -605,7 +606,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
                void* stream, mrt_trace_info* info) {
     if (!t) return fail(MRT_ERR_INVALID_ARG, "null tracer");
     if (numRays < 0) return fail(MRT_ERR_INVALID_ARG, "numRays < 0");
-    if (flags & ~0xFu) return fail(MRT_ERR_INVALID_ARG, "unknown trace flag");
+    if (flags & ~0x1Fu) return fail(MRT_ERR_INVALID_ARG, "unknown trace flag");
     std::lock_guard<std::mutex> lock(t->mu);
     if (info) std::memset(info, 0, sizeof(*info));
     if (numRays == 0) return MRT_OK;   // reference CudaTracer.cc:123-125: no rays => 0 ms
@@ -626,7 +627,10 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     const mrt_launch_cfg& uc = t->cfg;
     if (uc.autotune && uc.num_queues < 0 && uc.waves_per_cu == 0 && uc.fetch_threshold == 0 && uc.lane_groups == 1 &&
         !(flags & MRT_TRACE_STATS)) {
-        const auto key = std::make_pair(numRays, variant_key(v));
+        // secondary rays (MRT_TRACE_SECONDARY) settle their own schedule: a diffuse batch of a primary
+        // batch's size runs differently (round-5 README table: Mori primary 4829 Mrays/s on the diffuse
+        // batch's schedule, 5814 on its own)
+        const auto key = std::make_pair(numRays, variant_key(v) | ((flags & MRT_TRACE_SECONDARY) ? kSecondaryKey : 0));
         auto it = t->tunes.find(key);
         if (it != t->tunes.end()) {
             tune = it->second;

@@ -25,6 +25,7 @@ MRT_TRACE_ANY_HIT = 1 << 0
 MRT_TRACE_EXACT_RCP = 1 << 1
 MRT_TRACE_LOCKSTEP_OFF = 1 << 2
 MRT_TRACE_STATS = 1 << 3
+MRT_TRACE_SECONDARY = 1 << 4
 MRT_ERR_INVALID_ARG = 1
 MRT_ERR_STACK_OVERFLOW = 6
 

@@ -211,7 +211,7 @@ def trace_shard(tracer, rays, world: int, rank: int, max_rays: int = 1 << 21, ex
         return lo, hi
     from .tracer import RayBuffer
     local = RayBuffer(local_rays(rays.rays, shard_spans(rays.size, world, rank, block, owners, priority)),
-                      rays.need_closest_hit)
+                      rays.need_closest_hit, secondary=getattr(rays, "secondary", False))
     if stream is not None:
         # the local buffer was built on the current stream: the launches on `stream` wait for it
         stream.wait_stream(torch.cuda.current_stream())

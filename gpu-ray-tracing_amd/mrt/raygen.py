@@ -75,7 +75,7 @@ class DeviceRayGen:
         _lib.check(self.lib.mrt_raygen_ao(rays.rays.data_ptr() + 32 * first, rays.results.data_ptr() + 16 * first, n,
                                           self.normals.data_ptr(), self.num_tris, num_samples, float(max_dist),
                                           seed & 0xFFFFFFFF, out.data_ptr(), None, None, _stream_ptr(stream)))
-        return RayBuffer(out, need_closest_hit=closest_hit, device=self.device)
+        return RayBuffer(out, need_closest_hit=closest_hit, device=self.device, secondary=True)
 
     def count_hits_async(self, rays: RayBuffer, stream=None) -> torch.Tensor:
         """Device int32 scalar: results with id >= 0 (no host sync)."""

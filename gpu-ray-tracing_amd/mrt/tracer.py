@@ -64,9 +64,12 @@ class RayBuffer:
     needClosestHit selects the trace mode exactly like the reference
     (anyHit = !needClosestHit, CudaTracer.cc:172)."""
 
-    def __init__(self, rays, need_closest_hit: bool = True, device=None, results: torch.Tensor | None = None):
+    def __init__(self, rays, need_closest_hit: bool = True, device=None, results: torch.Tensor | None = None,
+                 secondary: bool = False):
         """results: an existing int32 [n, 4] device tensor to write into (e.g. a
-        slice of a larger RayResult array, for the shards of one RayBuffer)."""
+        slice of a larger RayResult array, for the shards of one RayBuffer).
+        secondary: the rays are AO / diffuse / later-bounce rays (a tuning hint, MRT_TRACE_SECONDARY:
+        the autotuner keeps their schedule apart from a primary batch of the same size)."""
         dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         if isinstance(rays, torch.Tensor):
             self.rays = rays.to(dev, torch.float32).contiguous().view(-1, 8)
@@ -79,11 +82,13 @@ class RayBuffer:
             raise ValueError("results must be a contiguous int32 [n, 4] tensor matching the rays")
         self.results = results
         self.need_closest_hit = need_closest_hit
+        self.secondary = bool(secondary)
         self.stats = None
 
     def view(self, lo: int, hi: int) -> "RayBuffer":
         """Rays [lo, hi) of this buffer as a RayBuffer sharing its rays and results."""
-        return RayBuffer(self.rays[lo:hi], self.need_closest_hit, self.rays.device, self.results[lo:hi])
+        return RayBuffer(self.rays[lo:hi], self.need_closest_hit, self.rays.device, self.results[lo:hi],
+                         secondary=self.secondary)
 
     @property
     def size(self) -> int:
@@ -165,6 +170,8 @@ class Tracer:
             f |= _lib.MRT_TRACE_LOCKSTEP_OFF
         if stats:
             f |= _lib.MRT_TRACE_STATS
+        if getattr(rays, "secondary", False):
+            f |= _lib.MRT_TRACE_SECONDARY
         return f
 
     def trace_async(self, rays: RayBuffer, exact_rcp=False, speculative=True, stats=False, stream=None) -> None:

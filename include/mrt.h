@@ -56,7 +56,10 @@ enum {
                                      default is the hardware v_rcp_f32 (the reference used rcp.approx)  */
     MRT_TRACE_LOCKSTEP_OFF = 1u << 2, /* per-lane (non-speculative) while-while: every lane follows the
                                      single-ray order exactly (deterministic any-hit, exact counters)  */
-    MRT_TRACE_STATS = 1u << 3     /* also write per-ray {inner nodes, tris tested, leaves, latency in 10 ns ticks} int4s */
+    MRT_TRACE_STATS = 1u << 3,    /* also write per-ray {inner nodes, tris tested, leaves, latency in 10 ns ticks} int4s */
+    MRT_TRACE_SECONDARY = 1u << 4 /* tuning hint, no effect on results: the batch holds secondary rays (AO, diffuse,
+                                     later bounces). The autotuner keeps their schedule apart from a primary batch
+                                     of the same size and kernel variant (saved / exported with variant | 512) */
 };
 
 /* One per HIP device. Re-entrant: launches on different streams get separate

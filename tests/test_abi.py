@@ -85,3 +85,24 @@ def test_cpp_dropin_resolves_the_reference_prototypes_from_libmrt():
     assert wanted <= set(line.split()[-1] for line in undef.splitlines() if line.strip())
     ldd = subprocess.run(["ldd", exe], capture_output=True, text=True, check=True).stdout
     assert "libmrt.so" in ldd and "not found" not in ldd.split("libmrt.so", 1)[1].splitlines()[0]
+
+
+def test_trace_flags_match_the_header():
+    """The Python flag constants are the header's enum values (MRT_TRACE_SECONDARY, round 5, included)."""
+    text = open(os.path.join(REPO, "include", "mrt.h")).read()
+    for name in ("MRT_TRACE_ANY_HIT", "MRT_TRACE_EXACT_RCP", "MRT_TRACE_LOCKSTEP_OFF", "MRT_TRACE_STATS",
+                 "MRT_TRACE_SECONDARY"):
+        m = re.search(name + r"\s*=\s*1u\s*<<\s*(\d+)", text)
+        assert m, name
+        assert getattr(_lib, name) == 1 << int(m.group(1)), name
+
+
+def test_secondary_hint_travels_with_the_buffer():
+    """RayBuffer.secondary reaches the trace flags and survives view() (no GPU needed)."""
+    import torch
+    from mrt.tracer import RayBuffer, Tracer
+    cpu = torch.device("cpu")
+    rb = RayBuffer(torch.zeros((8, 8)), need_closest_hit=True, device=cpu, secondary=True)
+    assert rb.view(2, 5).secondary
+    assert Tracer.flags(None, rb) & _lib.MRT_TRACE_SECONDARY
+    assert not Tracer.flags(None, RayBuffer(torch.zeros((8, 8)), device=cpu)) & _lib.MRT_TRACE_SECONDARY

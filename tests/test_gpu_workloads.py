@@ -220,6 +220,41 @@ def test_nearby_batch_sizes_and_other_streams_take_the_settled_schedule(env):
     tracer.set_bvh(e["gbvh"])
 
 
+def test_secondary_batches_keep_their_own_schedule(env):
+    """MRT_TRACE_SECONDARY (RayBuffer.secondary; DeviceRayGen.ao sets it): a batch of secondary
+    rays settles its own schedule even when a primary batch of the same size and kernel variant
+    has settled one (no inheritance across the two classes), and the two export as separate
+    entries (variant | 512). Results equal the oracle in both classes."""
+    from mrt.tracer import RayBuffer
+    bench, scenes, tracer, threads = env
+    name = "bunny-primary-640x480"
+    e = scenes.get(bench.workload_spec(name)[0])
+    bufs = scenes.host_buffers(bench.workload_spec(name)[0])
+    prim = bench.Batches(name, e["scene"], e["gbvh"], tracer).batches[0][0]
+    tracer.set_config(autotune=1)   # a fresh tuning state
+    sec = RayBuffer(prim.rays.clone(), need_closest_hit=True, secondary=True)
+    assert sec.view(0, 10).secondary and not prim.secondary
+    for _ in range(200):            # settle the primary class
+        tracer.trace_batch(prim, exact_rcp=True)
+        if tracer.last_info["autotune_locked"]:
+            break
+    assert tracer.last_info["autotune_locked"] == 1
+    tracer.trace_batch(sec, exact_rcp=True)   # same size and variant, the other class: it explores
+    assert tracer.last_info["autotune_locked"] == 0
+    for _ in range(200):
+        tracer.trace_batch(sec, exact_rcp=True)
+        if tracer.last_info["autotune_locked"]:
+            break
+    assert tracer.last_info["autotune_locked"] == 1
+    keys = {(n, v) for n, v, _, _ in tracer.schedules()}
+    v0 = next(v for n, v in keys if n == prim.size and not v & 512)
+    assert (prim.size, v0 | 512) in keys
+    want, _, _ = O.trace(prim.rays.cpu().numpy(), *bufs, threads=threads)
+    assert np.array_equal(prim.results_numpy()[:, :2], want[:, :2])
+    assert np.array_equal(sec.results_numpy()[:, :2], want[:, :2])
+    tracer.set_bvh(e["gbvh"])
+
+
 # SURVEY §8(a) Note 3 bounds: the "edge" class (an accept/reject flip of one triangle under
 # +-1 ulp of 1/Dz) at most 1e-6 of a workload's rays, and never more than one ray below 1e6 rays
 EDGE_FRACTION = 1e-6

@@ -52,7 +52,7 @@ def main():
     shards = []
     for k in range(world):
         rb = RayBuffer(local_rays(big, shard_spans(n, world, k, block, owners, prio)).contiguous(),
-                       need_closest_hit=True)
+                       need_closest_hit=True, secondary=True)
         shards.append((k, rb, int((rb.rays[:, 7] >= 0).sum())))
     torch.cuda.synchronize()
     if os.environ.get("TIMELINE"):
@@ -93,7 +93,8 @@ def main():
                   f"nodes/live {st[0] / max(1, live):.2f}", flush=True)
     import time
     from mrt.dist import shard_launches
-    whole = RayBuffer(local_rays(big, shard_spans(n, 1, 0, block, None, prio)).contiguous(), need_closest_hit=True)
+    whole = RayBuffer(local_rays(big, shard_spans(n, 1, 0, block, None, prio)).contiguous(), need_closest_hit=True,
+                      secondary=True)
     streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
     import json
     for item in filter(None, os.environ.get("EXTRA_SCHEDS", "").split(";")):

@@ -27,9 +27,11 @@ MARGIN = 0.03
 N_SCHEDULES, STAGE2 = 8, 5
 
 
-def variant_key(any_hit, exact, lds_stack=16, nodes=1, tail=False):
-    """mrt_api.cpp variant_key() of a speculative, stats-free launch."""
-    return int(any_hit) | 2 | (4 if exact else 0) | ({8: 0, 16: 1, 32: 2}[lds_stack] << 4) | (nodes << 6) | (256 if tail else 0)
+def variant_key(any_hit, exact, lds_stack=16, nodes=1, tail=False, secondary=False):
+    """mrt_api.cpp's tuning key of a speculative, stats-free launch: variant_key() | 512 for a
+    MRT_TRACE_SECONDARY batch."""
+    return (int(any_hit) | 2 | (4 if exact else 0) | ({8: 0, 16: 1, 32: 2}[lds_stack] << 4) | (nodes << 6)
+            | (256 if tail else 0) | (512 if secondary else 0))
 
 
 def main():
@@ -66,7 +68,8 @@ def main():
             launches = [tracer.launcher(rb, exact_rcp=exact) for rb, _ in b.batches]
             cfg = tracer.config()
             tail = cfg["tail_lanes"] > 0 and cfg["wide"] == 1   # the library's with_tail()
-            keys = sorted({(rb.size, variant_key(not rb.need_closest_hit, exact, tail=tail)) for rb, _ in b.batches})
+            keys = sorted({(rb.size, variant_key(not rb.need_closest_hit, exact, tail=tail, secondary=rb.secondary))
+                           for rb, _ in b.batches})
 
             def lock(code):
                 tracer.load_schedules([(n, v, code, _lib.MRT_TUNE_VERSION) for n, v in keys])
