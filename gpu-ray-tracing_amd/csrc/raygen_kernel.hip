@@ -91,6 +91,211 @@ __global__ __launch_bounds__(kThreads) void ao_per_sample_kernel(AOArgs a) {
     if (a.outSlotToId) a.outSlotToId[gid] = (int32_t)gid;
 }
 
+// A frame's secondary rays in block order (mrt_raygen_ao_blocks). The frame's
+// RayGen::batching sequence (RayGen.cc:124-142) numbers its rays g = p * S + i
+// (input ray p, sample i); batch k holds the inputs [k * P, (k + 1) * P) and hashes
+// seed_k + (p - k * P) (RayGen.cc:106, RayGenKernels.cu:122-134). Output ray j is
+// ray g = blocks[j / B] * B + j % B of that sequence, so a list of blocks in any
+// order comes out as the same bits the batches would hold at those positions —
+// a rank's shard generated directly in its trace order, no gather of a frame
+// buffer. One thread per output ray: consecutive lanes write consecutive 32-B
+// rays; a block id and an input ray are shared by B and S consecutive lanes.
+constexpr int kMaxBatchSeeds = 256;
+struct AOBlocksArgs {
+    const rg::RayRec* inRays;
+    const int2* inResults;
+    int numInput;
+    const float* normals;
+    int64_t numTris;
+    int numSamples;
+    float maxDist;
+    int batchInputs;          // P: input rays per batch
+    int blockRays;            // B
+    int64_t totalRays;        // numInput * numSamples
+    int64_t outRays;          // output rays of this launch
+    const int32_t* blocks;
+    rg::RayRec* out;
+    uint32_t seeds[kMaxBatchSeeds];
+};
+
+__global__ __launch_bounds__(kThreads) void ao_blocks_kernel(AOBlocksArgs a) {
+    const int64_t j = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (j >= a.outRays) return;
+    const int64_t k = j / a.blockRays;
+    const int64_t g = (int64_t)a.blocks[k] * a.blockRays + (j - k * a.blockRays);
+    if (g >= a.totalRays) return;   // past the frame's end: only the (last-listed) partial block
+    const int p = (int)(g / a.numSamples), i = (int)(g - (int64_t)p * a.numSamples);
+    const int batch = p / a.batchInputs;
+    const int2 res = a.inResults[2 * p];
+    const rg::AOBasis b = rg::ao_basis(a.inRays[p], res.x, __int_as_float(res.y), a.normals, a.numTris,
+                                       a.seeds[batch], (uint32_t)(p - batch * a.batchInputs));
+    a.out[j] = rg::ao_sample(b, i, a.maxDist);
+}
+
+// The same rays when a workgroup's kTileRays outputs lie inside one block (blockRays a
+// multiple of kTileRays) and hold whole input rays (numSamples divides kTileRays, at most
+// kThreads of them): each input ray's basis (two trig calls, a normalize, the hash, three
+// dependent loads) is computed once by one thread and each sample's hemisphere point once
+// per sample index, both through LDS — not once per output ray (S = 8: 8x fewer basis
+// evaluations) — then each thread writes kTileRays / kThreads rays (coalesced). Same
+// arithmetic, same bits. Four rays per thread: a 2 M-ray shard is 2 025 workgroups, one
+// round of the device, so the dependent load chain is paid once, not four times.
+constexpr int kTileRays = 1024;
+__global__ __launch_bounds__(kThreads) void ao_blocks_tiled_kernel(AOBlocksArgs a) {
+    __shared__ rg::AOBasis basis[kThreads];
+    __shared__ rg::V3 sample[kThreads];
+    const int t = (int)threadIdx.x;
+    const int64_t j0 = (int64_t)blockIdx.x * kTileRays;
+    const int64_t k = j0 / a.blockRays;
+    const int64_t g0 = (int64_t)a.blocks[k] * a.blockRays + (j0 - k * a.blockRays);   // a multiple of S
+    const int S = a.numSamples;
+    const int perWg = kTileRays / S;
+    const int p0 = (int)(g0 / S);
+    if (t < perWg && p0 + t < a.numInput) {
+        const int p = p0 + t;
+        const int batch = p / a.batchInputs;
+        const int2 res = a.inResults[2 * p];
+        basis[t] = rg::ao_basis(a.inRays[p], res.x, __int_as_float(res.y), a.normals, a.numTris, a.seeds[batch],
+                                (uint32_t)(p - batch * a.batchInputs));
+    }
+    if (kThreads - 1 - t < S) sample[kThreads - 1 - t] = rg::ao_sample_xyz(kThreads - 1 - t);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kTileRays / kThreads; u++) {
+        const int o = u * kThreads + t;
+        if (j0 + o >= a.outRays || g0 + o >= a.totalRays) break;
+        a.out[j0 + o] = rg::ao_sample_dir(basis[o / S], sample[o % S], a.maxDist);
+    }
+}
+
+// mrt_shard_blocks: a rank's blocks of the frame's secondary-ray order (block i to rank
+// i % world) and their trace order. Two launches, no host sync:
+//   block_live_kernel   one wave per listed block: its live rays = the samples of its input
+//                       rays whose primary hit (RayGenKernels.cu:117-227: a missed primary's
+//                       samples get tmax = -1), as the sort key B - live (the frame's partial
+//                       last block: the largest key, so it sorts last);
+//   block_order_kernel  one workgroup: a stable LSD radix sort of the list by that key in LDS
+//                       (three 4-bit digit passes; per-thread digit counts over contiguous chunks
+//                       keep equal keys in list = frame order), then the ordered block ids.
+constexpr int kOrderThreads = 1024;
+constexpr int kOrderMax = 16384;      // list entries the one-workgroup sort holds
+constexpr int kKeyMax = 4095;         // 12-bit keys
+
+struct ShardArgs {
+    const int2* results;     // primary RayResult viewed as int2 pairs
+    int numPrimary, numSamples, blockRays, world, rank, numBlocks;   // numBlocks: listed (this rank's)
+    int64_t totalRays;
+    int32_t* out;            // the block list; first the keys (block_live_kernel), then the ordered ids
+};
+
+__device__ inline int shard_block_id(const ShardArgs& a, int j) { return a.rank + j * a.world; }
+
+__global__ __launch_bounds__(kThreads) void block_live_kernel(ShardArgs a) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int j = (int)((blockIdx.x * kThreads + threadIdx.x) >> 6);
+    if (j >= a.numBlocks) return;
+    const int64_t g0 = (int64_t)shard_block_id(a, j) * a.blockRays;
+    const int64_t g1 = min(g0 + a.blockRays, a.totalRays);
+    const int64_t p0 = g0 / a.numSamples, p1 = (g1 - 1) / a.numSamples;   // input rays touching the block
+    int live = 0;
+    for (int64_t p = p0 + lane; p <= p1; p += 64) {
+        if (a.results[2 * p].x >= 0) {
+            const int64_t lo = max(g0, p * a.numSamples), hi = min(g1, (p + 1) * a.numSamples);
+            live += (int)(hi - lo);
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) live += __shfl_xor(live, off, 64);
+    if (lane == 0) {
+        int key = a.blockRays - live;   // decreasing live = increasing key
+        if (a.blockRays > kKeyMax - 1)  // quantized to 12 bits (mrt.dist.live_sort_key restates it)
+            key = (int)(((int64_t)key * (kKeyMax - 1) + a.blockRays - 1) / a.blockRays);
+        if (g1 - g0 < a.blockRays) key = kKeyMax;   // the partial last block sorts last
+        a.out[j] = key;
+    }
+}
+
+__global__ __launch_bounds__(kOrderThreads) void block_order_kernel(ShardArgs a) {
+    constexpr int kWaves = kOrderThreads / 64;
+    __shared__ uint16_t key[kOrderMax];
+    __shared__ uint16_t idx[2][kOrderMax];
+    __shared__ int waveTot[kWaves][16];
+    __shared__ int wavePre[kWaves][16];
+    static_assert((16 * kWaves) % 64 == 0, "the prefix wave walks (digit, wave) entries 64 at a time");
+    const int t = (int)threadIdx.x, lane = t & 63, wave = t >> 6, n = a.numBlocks;
+    for (int i = t; i < n; i += kOrderThreads) {
+        key[i] = (uint16_t)a.out[i];
+        idx[0][i] = (uint16_t)i;
+    }
+    const int chunk = (n + kOrderThreads - 1) / kOrderThreads;
+    const int lo = min(n, t * chunk), hi = min(n, lo + chunk);
+    int src = 0;
+    for (int shift = 0; shift < 12; shift += 4, src ^= 1) {
+        __syncthreads();
+        // this thread's digit counts over its contiguous chunk of the current order (registers:
+        // the digit selects by compare, no dynamic register indexing)
+        int c[16];
+#pragma unroll
+        for (int e = 0; e < 16; e++) c[e] = 0;
+        for (int i = lo; i < hi; i++) {
+            const int d = (key[idx[src][i]] >> shift) & 15;
+#pragma unroll
+            for (int e = 0; e < 16; e++) c[e] += d == e;
+        }
+        // exclusive offsets in (digit, thread) order: digit totals before d, plus this digit's
+        // counts of the threads before t — a wave scan per digit, the waves' totals through LDS,
+        // their (digit, wave) exclusive prefix by one wave, read back once per digit
+        int pre[16];
+#pragma unroll
+        for (int e = 0; e < 16; e++) {
+            int v = c[e];
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int u = __shfl_up(v, off, 64);
+                if (lane >= off) v += u;
+            }
+            pre[e] = v - c[e];
+            if (lane == 63) waveTot[wave][e] = v;
+        }
+        __syncthreads();
+        if (wave == 0) {   // lane l < 16 * kWaves / 64 ... one entry (digit e, wave w) per step, in order
+            int run = 0;
+            for (int e0 = 0; e0 < 16 * kWaves; e0 += 64) {
+                const int q = e0 + lane, e = q / kWaves, w = q - e * kWaves;
+                const int v = waveTot[w][e];
+                int incl = v;
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const int u = __shfl_up(incl, off, 64);
+                    if (lane >= off) incl += u;
+                }
+                wavePre[w][e] = run + incl - v;
+                run += __shfl(incl, 63, 64);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < 16; e++) pre[e] += wavePre[wave][e];
+        for (int i = lo; i < hi; i++) {
+            const uint16_t v = idx[src][i];
+            const int d = (key[v] >> shift) & 15;
+            int pos = 0;
+#pragma unroll
+            for (int e = 0; e < 16; e++) {
+                pos = d == e ? pre[e] : pos;
+                pre[e] += d == e;
+            }
+            idx[src ^ 1][pos] = v;
+        }
+    }
+    __syncthreads();
+    for (int i = t; i < n; i += kOrderThreads) a.out[i] = shard_block_id(a, idx[src][i]);
+}
+
+__global__ __launch_bounds__(kThreads) void block_list_kernel(ShardArgs a) {
+    const int j = (int)(blockIdx.x * kThreads + threadIdx.x);
+    if (j < a.numBlocks) a.out[j] = shard_block_id(a, j);
+}
+
 // Per block: hits among its rays (id >= 0, RendererKernels.cu:131), one partial.
 __global__ __launch_bounds__(kThreads) void count_partial_kernel(const int4* results, int n, int perBlock,
                                                                 int32_t* partial) {
@@ -290,6 +495,89 @@ int mrt_raygen_ao(const void* inRays, const void* inResults, int32_t numInputRay
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MRT_OK : hip_fail(e, "raygen ao launch");
+}
+
+int mrt_raygen_ao_blocks(const void* inRays, const void* inResults, int32_t numInputRays, const float* triNormals,
+                         int64_t numTris, int32_t numSamples, float maxDist, const uint32_t* batchSeeds,
+                         int32_t numBatches, int32_t batchInputRays, const int32_t* blocks, int32_t numBlocks,
+                         int32_t blockRays, int64_t numOutRays, void* outRays, void* stream) {
+    if (numInputRays < 0 || numSamples < 1 || numBlocks < 0 || blockRays < 1 || batchInputRays < 1 || numOutRays < 0)
+        return api_fail(MRT_ERR_INVALID_ARG, "bad ray/sample/block count");
+    const int64_t total = (int64_t)numInputRays * numSamples;
+    if (total > INT32_MAX) return api_fail(MRT_ERR_TOO_LARGE, "too many frame rays");
+    const int64_t needBatches = ((int64_t)numInputRays + batchInputRays - 1) / batchInputRays;
+    if (numBatches < needBatches) return api_fail(MRT_ERR_INVALID_ARG, "fewer batch seeds than batches");
+    if (needBatches > kMaxBatchSeeds) return api_fail(MRT_ERR_TOO_LARGE, "more than 256 batches in the frame");
+    const int64_t nb = (total + blockRays - 1) / blockRays;
+    if (numBlocks > nb) return api_fail(MRT_ERR_INVALID_ARG, "more blocks listed than the frame has");
+    if (numOutRays > (int64_t)numBlocks * blockRays || numOutRays < (int64_t)(numBlocks > 0 ? numBlocks - 1 : 0) * blockRays)
+        return api_fail(MRT_ERR_INVALID_ARG, "numOutRays does not match the listed blocks");
+    if (numOutRays == 0) return MRT_OK;
+    if (!inRays || !inResults || !outRays || !blocks || !batchSeeds || (numTris > 0 && !triNormals))
+        return api_fail(MRT_ERR_INVALID_ARG, "null argument");
+    AOBlocksArgs a{};
+    a.inRays = static_cast<const rg::RayRec*>(inRays);
+    a.inResults = static_cast<const int2*>(inResults);
+    a.numInput = numInputRays;
+    a.normals = triNormals;
+    a.numTris = numTris;
+    a.numSamples = numSamples;
+    a.maxDist = maxDist;
+    a.batchInputs = batchInputRays;
+    a.blockRays = blockRays;
+    a.totalRays = total;
+    a.outRays = numOutRays;
+    a.blocks = blocks;
+    a.out = static_cast<rg::RayRec*>(outRays);
+    for (int64_t k = 0; k < needBatches; k++) a.seeds[k] = batchSeeds[k];
+    if (blockRays % kTileRays == 0 && kTileRays % numSamples == 0 && kTileRays / numSamples <= kThreads)
+        hipLaunchKernelGGL(ao_blocks_tiled_kernel, dim3((unsigned)((numOutRays + kTileRays - 1) / kTileRays)),
+                           dim3(kThreads), 0, static_cast<hipStream_t>(stream), a);
+    else
+        hipLaunchKernelGGL(ao_blocks_kernel, dim3((unsigned)((numOutRays + kThreads - 1) / kThreads)), dim3(kThreads),
+                           0, static_cast<hipStream_t>(stream), a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MRT_OK : hip_fail(e, "raygen ao blocks launch");
+}
+
+int mrt_shard_blocks(const void* primaryResults, int32_t numPrimary, int32_t numSamples, int32_t blockRays,
+                     int32_t world, int32_t rank, int32_t order, int32_t* blocks, int32_t capacity, int32_t* numBlocks,
+                     int64_t* numRays, void* stream) {
+    if (numPrimary < 0 || numSamples < 1 || blockRays < 1 || world < 1 || rank < 0 || rank >= world ||
+        (order != 0 && order != 1) || !numBlocks || !numRays)
+        return api_fail(MRT_ERR_INVALID_ARG, "bad shard arguments");
+    const int64_t total = (int64_t)numPrimary * numSamples;
+    if (total > INT32_MAX) return api_fail(MRT_ERR_TOO_LARGE, "too many frame rays");
+    const int64_t nb = (total + blockRays - 1) / blockRays;
+    const int64_t mine = nb > rank ? (nb - 1 - rank) / world + 1 : 0;
+    const bool lastMine = mine > 0 && (nb - 1) % world == rank;
+    *numBlocks = (int32_t)mine;
+    *numRays = mine * blockRays - (lastMine ? nb * blockRays - total : 0);
+    if (mine == 0 || !blocks) return MRT_OK;   // blocks NULL: a size query
+    if (capacity < mine) return api_fail(MRT_ERR_TOO_LARGE, "block list capacity below the shard's blocks");
+    if (order == 1 && mine > kOrderMax)
+        return api_fail(MRT_ERR_TOO_LARGE, "live-first order holds at most 16384 blocks per rank (use larger blocks)");
+    if (order == 1 && !primaryResults) return api_fail(MRT_ERR_INVALID_ARG, "null primary results");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    ShardArgs a{};
+    a.results = static_cast<const int2*>(primaryResults);
+    a.numPrimary = numPrimary;
+    a.numSamples = numSamples;
+    a.blockRays = blockRays;
+    a.world = world;
+    a.rank = rank;
+    a.numBlocks = (int)mine;
+    a.totalRays = total;
+    a.out = blocks;
+    if (order == 0) {
+        hipLaunchKernelGGL(block_list_kernel, dim3((unsigned)((mine + kThreads - 1) / kThreads)), dim3(kThreads), 0, s, a);
+        const hipError_t e = hipGetLastError();
+        return e == hipSuccess ? MRT_OK : hip_fail(e, "shard block list launch");
+    }
+    hipLaunchKernelGGL(block_live_kernel, dim3((unsigned)((mine * 64 + kThreads - 1) / kThreads)), dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL(block_order_kernel, dim3(1), dim3(kOrderThreads), 0, s, a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MRT_OK : hip_fail(e, "shard order launch");
 }
 
 int mrt_count_hits(const void* results, int32_t numRays, int32_t* hitCount, void* stream) {

@@ -98,6 +98,8 @@ TRACE_SYMBOLS = [
     ("mrt_raygen_primary_subpixel", i32, [C.POINTER(f32), C.POINTER(f32), f32, i32, i32, f32, f32, vp, vp, vp, vp,
                                           vp]),
     ("mrt_raygen_ao", i32, [vp, vp, i32, vp, i64, i32, f32, u32, vp, vp, vp, vp]),
+    ("mrt_raygen_ao_blocks", i32, [vp, vp, i32, vp, i64, i32, f32, vp, i32, i32, vp, i32, i32, i64, vp, vp]),
+    ("mrt_shard_blocks", i32, [vp, i32, i32, i32, i32, i32, i32, vp, i32, C.POINTER(i32), C.POINTER(i64), vp]),
     ("mrt_count_hits", i32, [vp, i32, vp, vp]),
     ("mrt_reconstruct", i32, [i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp]),
     ("mrt_selftest_exact_rcp", i32, [C.POINTER(C.c_uint64)]),

@@ -77,6 +77,97 @@ def balance_blocks(weights, world: int) -> np.ndarray:
     return owners
 
 
+def shard_blocks(n: int, world: int, rank: int, block: int, owners=None, priority=None) -> np.ndarray:
+    """The block ids (int64) of `rank`'s block-cyclic shard of n rays in trace order:
+    block i to rank i % world (or owners[i]), in frame order or, with priority (one value
+    >= 0 per block, e.g. block_weights), in decreasing priority (ties in frame order). The
+    frame's last block, when partial (n % block != 0), always comes last, so a shard's
+    rays are whole blocks followed by at most one short one (what mrt_raygen_ao_blocks
+    generates)."""
+    if block <= 0:
+        raise ValueError("shard_blocks: block must be positive")
+    nblocks = -(-n // block)
+    if owners is not None:
+        owners = np.asarray(owners)
+        if len(owners) != nblocks:
+            raise ValueError(f"shard_spans: {len(owners)} block owners for {nblocks} blocks of {block} rays")
+        mine = np.flatnonzero(owners == rank)
+    else:
+        mine = np.arange(rank, nblocks, world)
+    if priority is not None and len(mine):
+        pr = np.asarray(priority.cpu() if isinstance(priority, torch.Tensor) else priority)
+        if len(pr) != nblocks:
+            raise ValueError(f"shard_spans: {len(pr)} block priorities for {nblocks} blocks of {block} rays")
+        key = -np.asarray(pr[mine], dtype=np.float64)
+        if n % block:
+            key[mine == nblocks - 1] = np.inf     # the partial block last
+        mine = mine[np.argsort(key, kind="stable")]
+    return mine.astype(np.int64)
+
+
+def shard_blocks_device(n: int, world: int, rank: int, block: int, owners=None, priority=None, device=None):
+    """shard_blocks on the device, without a host sync: (int32 block ids on `device`, the
+    number of rays they hold). priority: a device tensor (e.g. live_block_weights); the
+    order is shard_blocks' (a stable sort of the same keys), so gather_results /
+    shard_spans with the same priority on the host put the results back."""
+    nblocks = -(-n // block)
+    if owners is not None:
+        mine_h = np.flatnonzero(np.asarray(owners) == rank)
+    else:
+        mine_h = np.arange(rank, nblocks, world)
+    partial = n % block
+    last_mine = len(mine_h) > 0 and int(mine_h[-1]) == nblocks - 1
+    num_rays = len(mine_h) * block - ((block - partial) if partial and last_mine else 0)
+    mine = (torch.from_numpy(mine_h).to(device) if owners is not None
+            else torch.arange(rank, nblocks, world, dtype=torch.int64, device=device))
+    if priority is not None and len(mine_h):
+        if priority.numel() != nblocks:
+            raise ValueError(f"shard_blocks_device: {priority.numel()} block priorities for {nblocks} blocks")
+        key = -priority.to(device)[mine].to(torch.float64)
+        if partial and last_mine:
+            key = torch.where(mine == nblocks - 1, torch.full_like(key, float("inf")), key)
+        mine = mine[torch.argsort(key, stable=True)]
+    return mine.to(torch.int32), int(num_rays)
+
+
+def live_block_weights(primary_results: torch.Tensor, num_samples: int, block: int) -> torch.Tensor:
+    """block_weights of a frame's AO/diffuse rays known before they exist: a secondary ray
+    is live (tmax >= 0) exactly when its primary ray hit (RayGenKernels.cu:117-227), so the
+    live rays per block-ray block of the frame's ray order (input p's samples at p*S..)
+    follow from the primary pass's results (RayResult int32 [n, 4]) — one reduction on
+    their device, int64 [ceil(n*S / block)]."""
+    if block <= 0 or num_samples < 1:
+        raise ValueError("live_block_weights: block and num_samples must be positive")
+    hit = (primary_results[:, 0] >= 0).to(torch.int64)
+    total = hit.numel() * num_samples
+    nblocks = -(-total // block)
+    if block % num_samples == 0:
+        per = block // num_samples
+        pad = nblocks * per - hit.numel()
+        if pad:
+            hit = torch.cat([hit, hit.new_zeros(pad)])
+        return hit.view(-1, per).sum(1) * num_samples
+    live = hit.repeat_interleave(num_samples)
+    pad = nblocks * block - total
+    if pad:
+        live = torch.cat([live, live.new_zeros(pad)])
+    return live.view(-1, block).sum(1)
+
+
+KEY_MAX = 4094   # mrt_shard_blocks' live-order keys: 12 bits (4095 = the partial last block)
+
+
+def live_priority(weights, block: int) -> np.ndarray:
+    """The host priority (for shard_blocks / shard_spans / gather_results) whose order is
+    mrt_shard_blocks' live-first order: decreasing live count, quantized to mrt_shard_blocks'
+    12-bit key when block > 4094 (key = ceil((block - live) * 4094 / block))."""
+    w = np.asarray(weights.cpu() if isinstance(weights, torch.Tensor) else weights, dtype=np.int64)
+    key = block - w
+    if block > KEY_MAX:
+        key = (key * KEY_MAX + block - 1) // block
+    return -key
+
+
 def shard_spans(n: int, world: int, rank: int, block: int = 0, owners=None, priority=None) -> list[tuple[int, int]]:
     """The ray ranges of `rank`'s shard of n rays. block = 0: one contiguous range
     (shard_range). block > 0: block-cyclic — the buffer cut into block-ray blocks,
@@ -87,29 +178,18 @@ def shard_spans(n: int, world: int, rank: int, block: int = 0, owners=None, prio
     0.59-1.12 ms on one MI355X, which caps eta(8) at 0.54. owners (block > 0):
     block i to rank owners[i] instead (balance_blocks). priority (block > 0, one
     value per block, e.g. block_weights): the rank's blocks in decreasing priority
-    (ties in frame order) instead of frame order, so a launch that deals its rays in
-    order starts its costly blocks first and ends on the cheap ones (with world = 1:
-    the whole buffer reordered). Blocks adjacent in the result are merged."""
-    nblocks = -(-n // block) if block > 0 else 0
+    (ties in frame order, a partial last block last: shard_blocks) instead of frame
+    order, so a launch that deals its rays in order starts its costly blocks first
+    and ends on the cheap ones (with world = 1: the whole buffer reordered). Blocks
+    adjacent in the result are merged."""
     if block <= 0 or (world == 1 and priority is None):
         lo, hi = shard_range(n, world, rank)
         return [(lo, hi)] if hi > lo else []
-    if owners is not None:
-        owners = np.asarray(owners)
-        if len(owners) != nblocks:
-            raise ValueError(f"shard_spans: {len(owners)} block owners for {nblocks} blocks of {block} rays")
-        mine = np.flatnonzero(owners == rank)
-    else:
-        mine = np.arange(rank, nblocks, world)
-    if priority is not None:
-        pr = np.asarray(priority.cpu() if isinstance(priority, torch.Tensor) else priority)
-        if len(pr) != nblocks:
-            raise ValueError(f"shard_spans: {len(pr)} block priorities for {nblocks} blocks of {block} rays")
-        mine = mine[np.argsort(-pr[mine], kind="stable")]
+    mine = shard_blocks(n, world, rank, block, owners, priority)
     if len(mine) == 0:
         return []
     # the blocks' ranges, adjacent ones merged (vectorised: a 16.6 M-ray buffer has 16 k blocks)
-    starts = mine.astype(np.int64) * block
+    starts = mine * block
     ends = np.minimum(n, starts + block)
     first = np.ones(len(mine), bool)
     first[1:] = starts[1:] != ends[:-1]

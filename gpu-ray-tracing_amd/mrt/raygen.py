@@ -77,6 +77,44 @@ class DeviceRayGen:
                                           seed & 0xFFFFFFFF, out.data_ptr(), None, None, _stream_ptr(stream)))
         return RayBuffer(out, need_closest_hit=closest_hit, device=self.device, secondary=True)
 
+    def ao_blocks(self, rays: RayBuffer, num_samples: int, max_dist: float, seeds, batch_inputs: int,
+                  blocks: torch.Tensor, block_rays: int, num_rays: int, closest_hit: bool = False,
+                  stream=None) -> RayBuffer:
+        """The frame's AO/diffuse rays for a list of blocks of its ray order (mrt_raygen_ao_blocks):
+        the rays RayGen::batching's batches (batch_inputs input rays each, seeded by seeds[k])
+        hold at positions blocks[i] * block_rays + [0, block_rays), concatenated in list order —
+        e.g. one rank's shard of the frame in its trace order, generated directly. blocks: int32
+        device tensor; num_rays: the rays listed (a partial last block of the frame, when listed,
+        must be the last entry: mrt.dist.shard_blocks_device keeps it there)."""
+        if self.normals is None:
+            raise _lib.MrtError("DeviceRayGen.ao_blocks needs the scene's triangle normals (pass scene=)")
+        if blocks.dtype != torch.int32 or blocks.dim() != 1 or blocks.device != torch.device(self.device):
+            raise _lib.MrtError("ao_blocks: blocks must be a 1-D int32 tensor on the generator's device")
+        sd = (C.c_uint32 * max(1, len(seeds)))(*[s & 0xFFFFFFFF for s in seeds])
+        out = torch.empty((num_rays, 8), dtype=torch.float32, device=self.device)
+        _lib.check(self.lib.mrt_raygen_ao_blocks(rays.rays.data_ptr(), rays.results.data_ptr(), rays.size,
+                                                 self.normals.data_ptr(), self.num_tris, num_samples, float(max_dist),
+                                                 C.cast(sd, C.c_void_p), len(seeds), batch_inputs, blocks.data_ptr(),
+                                                 blocks.numel(), block_rays, num_rays, out.data_ptr(),
+                                                 _stream_ptr(stream)))
+        return RayBuffer(out, need_closest_hit=closest_hit, device=self.device, secondary=True)
+
+    def shard_blocks(self, primary: RayBuffer, num_samples: int, block_rays: int, world: int, rank: int,
+                     order: int = 1, stream=None) -> tuple[torch.Tensor, int]:
+        """mrt_shard_blocks: rank's blocks (block i to rank i % world) of the frame's AO/diffuse
+        ray order, in frame order (order 0) or live blocks first (1: decreasing live rays from
+        the primary pass's results, ties in frame order, a partial last block last), as an int32
+        device tensor, and the rays they hold — two small launches, no host sync."""
+        n = C.c_int32(0)
+        m = C.c_int64(0)
+        _lib.check(self.lib.mrt_shard_blocks(None, primary.size, num_samples, block_rays, world, rank, 0, None, 0,
+                                             C.byref(n), C.byref(m), None))
+        blocks = torch.empty(max(1, n.value), dtype=torch.int32, device=self.device)
+        _lib.check(self.lib.mrt_shard_blocks(primary.results.data_ptr(), primary.size, num_samples, block_rays, world,
+                                             rank, order, blocks.data_ptr(), blocks.numel(), C.byref(n), C.byref(m),
+                                             _stream_ptr(stream)))
+        return blocks[:n.value], m.value
+
     def count_hits_async(self, rays: RayBuffer, stream=None) -> torch.Tensor:
         """Device int32 scalar: results with id >= 0 (no host sync)."""
         out = torch.empty(1, dtype=torch.int32, device=self.device)

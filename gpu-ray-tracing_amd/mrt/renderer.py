@@ -82,6 +82,7 @@ class Renderer:
         self.batch_start = 0      # first ray of the current batch in the frame's secondary-ray sequence
         self._next_input = 0      # RayGen's m_aoStartIdx
         self._new_batch = True
+        self._seeds: list[int] = []   # this frame's batch seeds, drawn from rand() in batch order
 
     def set_params(self, ray_type: int = RAY_PRIMARY, num_samples: int = 1, ao_radius: float = 5.0) -> None:
         if ray_type not in (RAY_PRIMARY, RAY_AO, RAY_DIFFUSE):
@@ -94,6 +95,7 @@ class Renderer:
         if self.ray_type != RAY_PRIMARY:
             self.tracer.trace_batch(self.primary, exact_rcp=self.exact_rcp)
         self.batch, self.batch_start, self._next_input, self._new_batch = None, 0, 0, True
+        self._seeds = []
 
     def total_num_rays(self) -> int:
         if self.ray_type == RAY_PRIMARY:
@@ -115,10 +117,52 @@ class Renderer:
             return False
         lo, hi = rng
         self._next_input = hi
-        dist = self.ao_radius if self.ray_type == RAY_AO else self.cam.far
-        self.batch = self.gen.ao(self.primary, self.num_samples, dist, seed=self.rand(),
+        self.batch = self.gen.ao(self.primary, self.num_samples, self._max_dist(),
+                                 seed=self.batch_seeds(lo // self._batch_inputs() + 1)[-1],
                                  closest_hit=self.ray_type == RAY_DIFFUSE, first=lo, count=hi - lo)
         return True
+
+    def _max_dist(self) -> float:
+        return self.ao_radius if self.ray_type == RAY_AO else self.cam.far
+
+    def _batch_inputs(self) -> int:
+        return self.max_batch // self.num_samples      # RayGen::batching's primaries per batch
+
+    def num_batches(self) -> int:
+        """Secondary batches of the frame (RayGen::batching, RayGen.cc:124-142)."""
+        return -(-self.primary.size // self._batch_inputs()) if self.ray_type != RAY_PRIMARY else 1
+
+    def batch_seeds(self, count: int | None = None) -> list[int]:
+        """The seeds of the frame's first `count` (default: all) secondary batches: one
+        rand() per batch in batch order (RayGen.cc:106), drawn once per frame and shared by
+        next_batch and secondary_blocks, so both see the same sequence."""
+        count = self.num_batches() if count is None else count
+        while len(self._seeds) < count:
+            self._seeds.append(self.rand())
+        return self._seeds[:count]
+
+    def secondary_blocks(self, blocks: torch.Tensor, num_rays: int, block_rays: int, stream=None) -> RayBuffer:
+        """The frame's AO/diffuse rays at a list of block_rays-ray blocks of its ray order
+        (the order next_batch's batches hold them in), generated directly in list order on the
+        device (mrt_raygen_ao_blocks) — a rank's shard of the frame, or the whole frame with
+        its costly blocks first, with no frame-order buffer and no gather. Bit-identical to
+        the same positions of the batches. num_rays: the rays listed (mrt.dist.shard_blocks_device)."""
+        if self.ray_type == RAY_PRIMARY or self.primary is None:
+            raise _lib.MrtError("secondary_blocks needs an AO or diffuse frame (set_params, begin_frame)")
+        return self.gen.ao_blocks(self.primary, self.num_samples, self._max_dist(), self.batch_seeds(),
+                                  self._batch_inputs(), blocks, block_rays, num_rays,
+                                  closest_hit=self.ray_type == RAY_DIFFUSE, stream=stream)
+
+    def shard(self, world: int, rank: int, block_rays: int, order: int = 1, stream=None) -> RayBuffer:
+        """Rank's shard of the frame's AO/diffuse rays for a world-rank job, generated in its
+        trace order on the device: block i of block_rays rays to rank i % world, live blocks
+        first (order 1) or in frame order (0) — mrt_shard_blocks, then secondary_blocks. Two
+        ranks' shards hold disjoint rays; together, the frame (mrt.dist.gather_results with
+        block=block_rays and priority=mrt.dist.live_priority(...) puts results back)."""
+        if self.ray_type == RAY_PRIMARY or self.primary is None:
+            raise _lib.MrtError("shard needs an AO or diffuse frame (set_params, begin_frame)")
+        blocks, n = self.gen.shard_blocks(self.primary, self.num_samples, block_rays, world, rank, order, stream)
+        return self.secondary_blocks(blocks, n, block_rays, stream)
 
     def trace_batch(self) -> float:
         if self.batch is None:

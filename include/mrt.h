@@ -277,6 +277,35 @@ int  mrt_raygen_ao(const void* inRays, const void* inResults, int32_t numInputRa
                    int64_t numTris, int32_t numSamples, float maxDist, uint32_t seed, void* outRays,
                    int32_t* outIdToSlot, int32_t* outSlotToId, void* stream);
 
+/* A whole frame's AO/diffuse rays, generated for a list of blocks of the frame's ray order
+ * instead of batch by batch: the frame's RayGen::batching sequence (RayGen.cc:124-142) —
+ * batch k = input rays [k*batchInputRays, (k+1)*batchInputRays), seeded by batchSeeds[k]
+ * (host array, one glibc rand() per batch, RayGen.cc:106), numSamples rays per input ray
+ * — numbers its rays g = input * numSamples + sample; output ray j is ray
+ * blocks[j / blockRays] * blockRays + j % blockRays of it, bit-identical to the ray the
+ * batches hold there (mrt_raygen_ao of batch k). blocks: device int32[numBlocks], any
+ * order (e.g. a rank's shard, its costly blocks first). Only the frame's last block can
+ * be partial; when listed it must be the last entry, and numOutRays = the listed rays
+ * ((numBlocks-1)*blockRays + its length; else numBlocks*blockRays). At most 256 batches. */
+int  mrt_raygen_ao_blocks(const void* inRays, const void* inResults, int32_t numInputRays, const float* triNormals,
+                          int64_t numTris, int32_t numSamples, float maxDist, const uint32_t* batchSeeds,
+                          int32_t numBatches, int32_t batchInputRays, const int32_t* blocks, int32_t numBlocks,
+                          int32_t blockRays, int64_t numOutRays, void* outRays, void* stream);
+
+/* One rank's blocks of a frame's AO/diffuse ray order for mrt_raygen_ao_blocks (multi-GPU
+ * sharding: no reference counterpart — the reference is single-GPU). The frame's
+ * numPrimary*numSamples rays are cut into blockRays-ray blocks, block i to rank i % world;
+ * order 0 lists the rank's blocks in frame order, order 1 live blocks first: decreasing
+ * number of live rays (samples whose primary ray hit, read from primaryResults — the primary
+ * pass's RayResult[numPrimary]; a missed primary's samples are degenerate, tmax = -1), ties in
+ * frame order, the frame's partial last block last (live counts quantized to 12 bits when
+ * blockRays > 4094; order 1 holds at most 16384 blocks per rank). blocks: device
+ * int32[capacity] (NULL: only *numBlocks / *numRays are set); *numBlocks and *numRays (host) =
+ * the rank's blocks and the rays they hold, known without the device. Stream-ordered, no host sync. */
+int  mrt_shard_blocks(const void* primaryResults, int32_t numPrimary, int32_t numSamples, int32_t blockRays,
+                      int32_t world, int32_t rank, int32_t order, int32_t* blocks, int32_t capacity,
+                      int32_t* numBlocks, int64_t* numRays, void* stream);
+
 /* countHitsKernel (RendererKernels.cu:112-162): *hitCount (device int32) = number of
  * results with id >= 0. */
 int  mrt_count_hits(const void* results, int32_t numRays, int32_t* hitCount, void* stream);

@@ -155,4 +155,58 @@ def test_block_sums_and_weights():
     rays[[0, 5, 9], 7] = -1.0
     assert block_weights(rays, 4).tolist() == [3, 3, 1]
     spans = shard_spans(10, 1, 0, 4, priority=block_sums(v, 4))
-    assert spans == [(4, 10), (0, 4)]   # costliest block first (adjacent blocks 1, 2 merged)
+    assert spans == [(4, 8), (0, 4), (8, 10)]   # costliest block first, the partial last block last
+    assert shard_spans(12, 1, 0, 4, priority=[6, 22, 17]) == [(4, 12), (0, 4)]   # adjacent blocks 1, 2 merged
+
+
+def test_live_block_weights_follow_the_primary_hits():
+    """live_block_weights: a frame's secondary ray is live (tmax >= 0) iff its primary ray hit
+    (RayGenKernels.cu:117-227), so the live count per block of the frame's ray order is known
+    from the primary results: equal to block_weights of the generated rays, for block sizes
+    that are and are not multiples of the samples, with a partial last block."""
+    from mrt.dist import block_weights, live_block_weights
+    g = torch.Generator().manual_seed(5)
+    for n_prim, spp, block in ((37, 4, 8), (37, 3, 8), (50, 1, 7), (64, 8, 64), (5, 2, 64)):
+        res = torch.zeros((n_prim, 4), dtype=torch.int32)
+        res[:, 0] = torch.where(torch.rand(n_prim, generator=g) < 0.6, torch.randint(0, 9, (n_prim,), generator=g), -1)
+        rays = torch.zeros((n_prim * spp, 8))
+        rays[:, 7] = torch.where(res[:, 0] >= 0, 100.0, -1.0).repeat_interleave(spp)
+        assert live_block_weights(res, spp, block).tolist() == block_weights(rays, block).tolist()
+
+
+@pytest.mark.parametrize("n,block,world", [(1000, 64, 3), (1024, 64, 4), (17, 5, 2), (64, 64, 2)])
+def test_shard_blocks_device_matches_the_host_order(n, block, world):
+    """shard_blocks_device (the device deal used to generate shards) equals shard_blocks and
+    shard_spans on the host for the same priorities: every rank's blocks in the same order,
+    the ray counts right, the partial block last, every ray in exactly one shard."""
+    from mrt.dist import shard_blocks, shard_blocks_device, spans_index
+    nb = -(-n // block)
+    pr = np.random.RandomState(n).randint(0, 5, size=nb)
+    seen = np.zeros(n, int)
+    for prio in (None, pr):
+        for r in range(world):
+            host = shard_blocks(n, world, r, block, priority=prio)
+            dev, m = shard_blocks_device(n, world, r, block, priority=None if prio is None else torch.tensor(prio))
+            assert dev.dtype == torch.int32 and np.array_equal(dev.numpy(), host)
+            if n % block and (nb - 1) in host:
+                assert host[-1] == nb - 1
+            idx = spans_index(shard_spans(n, world, r, block, None, prio)).numpy()
+            assert len(idx) == m
+            if prio is not None:
+                seen[idx] += 1
+    assert (seen == 1).all()
+
+
+def test_partial_block_last_with_negative_priorities():
+    """live_priority's values are <= 0: the frame's partial last block still comes last."""
+    from mrt.dist import live_priority, shard_blocks, shard_blocks_device
+    n, block = 17751, 128
+    nb = -(-n // block)
+    w = np.random.RandomState(3).randint(0, block + 1, size=nb)
+    pr = live_priority(w, block)
+    for r in range(2):
+        host = shard_blocks(n, 2, r, block, priority=pr)
+        dev, _ = shard_blocks_device(n, 2, r, block, priority=torch.from_numpy(pr))
+        assert np.array_equal(host, dev.numpy())
+        if (nb - 1) % 2 == r:
+            assert host[-1] == nb - 1

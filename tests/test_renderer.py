@@ -147,3 +147,86 @@ def test_renderer_batches_equal_the_oracle(sponza, ray_type, samples, w, h):
     want_px = O.reconstruct(ray_type, samples, r.slot_to_id.cpu().numpy(), prim_res, np.concatenate(bres), mat, sh,
                             w * h)
     assert np.array_equal(pixels.cpu().numpy().view(np.uint32), want_px)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ray_type,samples,w,h,max_batch,block,world", [
+    (2, 8, 320, 240, 1 << 16, 1024, 3),     # 10 batches; blocks a multiple of the samples
+    (1, 3, 97, 61, 1 << 12, 100, 2),        # ragged: 3 samples, 100-ray blocks, a partial last block
+    (2, 1, 160, 120, 1 << 21, 4096, 1),     # one batch, the whole frame live blocks first
+])
+def test_secondary_blocks_equal_the_frame_batches(sponza, ray_type, samples, w, h, max_batch, block, world):
+    """Renderer.secondary_blocks (mrt_raygen_ao_blocks): each rank's shard of
+    the frame generated directly in its trace order (live blocks first) is bit-identical to
+    the frame's RayGen::batching batches gathered at the shard's blocks, and the shards
+    together hold every ray of the frame once. The live counts per block from the primary
+    pass equal the generated rays' own (tmax >= 0)."""
+    from mrt.dist import block_weights, live_block_weights, shard_blocks_device, shard_spans, spans_index
+    from mrt.renderer import Renderer
+    scene, bufs, t = sponza
+    cam, ao = scene.camera()
+    r = Renderer(t, scene, max_batch=max_batch)
+    r.set_params(ray_type, samples, ao)
+    r.begin_frame(cam, w, h)
+    n = w * h * samples
+    frame = torch.cat([b.rays for b, _ in r.batches()])      # seeds drawn here, in batch order
+    assert frame.shape[0] == n and r.num_batches() == -(-w * h // (max_batch // samples))
+    wdev = live_block_weights(r.primary.results, samples, block)
+    assert torch.equal(wdev.cpu(), block_weights(frame, block).cpu())
+    prio = wdev.cpu().numpy()
+    seen = torch.zeros(n, dtype=torch.int32, device="cuda")
+    for rank in range(world):
+        blocks, m = shard_blocks_device(n, world, rank, block, priority=wdev, device="cuda")
+        shard = r.secondary_blocks(blocks, m, block)
+        assert shard.secondary and shard.need_closest_hit == (ray_type == 2)
+        idx = spans_index(shard_spans(n, world, rank, block, None, prio), "cuda")
+        assert shard.size == m == idx.numel()
+        assert torch.equal(shard.rays, frame.index_select(0, idx)), f"rank {rank}: shard rays differ"
+        seen.index_add_(0, idx, torch.ones_like(idx, dtype=torch.int32))
+    assert bool((seen == 1).all())
+
+
+@pytest.mark.gpu
+def test_secondary_blocks_rejects_bad_lists(sponza):
+    from mrt.renderer import Renderer
+    scene, _, t = sponza
+    cam, ao = scene.camera()
+    r = Renderer(t, scene)
+    r.set_params(1, 2, ao)
+    r.begin_frame(cam, 32, 32)
+    blocks = torch.arange(0, 8, dtype=torch.int32, device="cuda")
+    with pytest.raises(mrt._lib.MrtError):
+        r.secondary_blocks(blocks, 8 * 64 + 1, 64)           # more rays than the blocks hold
+    with pytest.raises(mrt._lib.MrtError):
+        r.secondary_blocks(torch.arange(0, 40, dtype=torch.int32, device="cuda"), 40 * 64, 64)   # > the frame's 32
+    out = r.secondary_blocks(blocks[:0], 0, 64)
+    assert out.size == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("samples,w,h,block,world", [(8, 320, 240, 1024, 3), (3, 97, 61, 128, 2), (1, 160, 120, 4096, 1),
+                                                    (2, 200, 100, 8192, 2)])
+def test_library_shard_order_equals_the_host_deal(sponza, samples, w, h, block, world):
+    """mrt_shard_blocks (Renderer.shard): every rank's blocks, in frame order and live blocks
+    first, equal the host's deal (shard_blocks with live_priority — the gather's spans), and the
+    shard's rays equal the frame's batches at those positions; a 8192-ray block exercises the
+    quantized keys."""
+    from mrt.dist import live_block_weights, live_priority, shard_blocks, shard_spans, spans_index
+    from mrt.renderer import Renderer
+    scene, bufs, t = sponza
+    cam, ao = scene.camera()
+    r = Renderer(t, scene, max_batch=1 << 15)
+    r.set_params(2, samples, ao)
+    r.begin_frame(cam, w, h)
+    n = w * h * samples
+    frame = torch.cat([b.rays for b, _ in r.batches()])
+    prio = live_priority(live_block_weights(r.primary.results, samples, block).cpu(), block)
+    for order in (0, 1):
+        for rank in range(world):
+            blocks, m = r.gen.shard_blocks(r.primary, samples, block, world, rank, order)
+            want = shard_blocks(n, world, rank, block, priority=prio if order else None)
+            assert np.array_equal(blocks.cpu().numpy(), want), f"order {order} rank {rank}"
+            shard = r.shard(world, rank, block, order=order)
+            idx = spans_index(shard_spans(n, world, rank, block, None, prio if order else None), "cuda")
+            assert shard.size == m == idx.numel()
+            assert torch.equal(shard.rays, frame.index_select(0, idx))

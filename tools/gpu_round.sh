@@ -69,6 +69,12 @@ for step in "$@"; do
       P="$P;SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL SQ_ACTIVE_INST_VMEM TA_ADDR_STALLED_BY_TC_CYCLES_sum TA_DATA_STALLED_BY_TC_CYCLES_sum GRBM_GUI_ACTIVE"
       timeout -k 10 900 bash tools/pmc_pipe.sh $arg $O/pipe_$arg "$P" > $O/pipe_$arg.log 2>&1 || fail "pipe $arg" $O/pipe_$arg.log
       python3 tools/pipe_summary.py $O/pipe_$arg > $O/pipe_$arg.txt && tail -12 $O/pipe_$arg.txt ;;
+    tlb)   # address translation (UTCL1 hits/misses, UTCL2 busy) + L1->L2 requests of workload W (3 PMC passes)
+      P="TCP_UTCL1_REQUEST_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_STALL_MULTI_MISS_sum GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE"
+      P="$P;TCP_UTCL1_TRANSLATION_MISS_UNDER_MISS_sum TCP_UTCL1_SERIALIZATION_STALL_sum TCP_UTCL1_STALL_LFIFO_NO_RES_sum TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum GRBM_GUI_ACTIVE"
+      P="$P;TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_PENDING_STALL_CYCLES_sum GRBM_GUI_ACTIVE"
+      timeout -k 10 900 bash tools/pmc_pipe.sh $arg $O/tlb_$arg "$P" > $O/tlb_$arg.log 2>&1 || fail "tlb $arg" $O/tlb_$arg.log
+      python3 tools/pipe_summary.py $O/tlb_$arg > $O/tlb_$arg.txt && tail -14 $O/tlb_$arg.txt ;;
     timeline)
       MRT_LIB_DIR=$PWD/gpu-ray-tracing_amd/lib/variants/tailtl timeout -k 10 300 python -u tools/tail_timeline.py $arg \
         '{"tail_lanes": 0, "autotune": 0}' '{"tail_lanes": 16, "autotune": 0}' >> $O/tail_tl.txt 2>> $O/tail_tl.err || fail timeline $O/tail_tl.err

@@ -36,6 +36,20 @@ def main():
                   "TCP_TCP_TA_DATA_STALL_CYCLES_sum", "TD_TD_BUSY_sum", "TD_TC_STALL_sum"):
             if k in c:
                 print(f"{k:40s} per CU per cycle {c[k] / cus / cyc:8.3f}")
+    if "TCP_UTCL1_REQUEST_sum" in c:
+        req = c["TCP_UTCL1_REQUEST_sum"]
+        miss = c.get("TCP_UTCL1_TRANSLATION_MISS_sum", 0.0)
+        print(f"UTCL1 translation miss rate (MISS / REQUEST)   {miss / max(req, 1.0):12.4f}")
+        if "TCP_TCC_READ_REQ_sum" in c:
+            print(f"UTCL1 misses per L1->L2 line request          {miss / max(c['TCP_TCC_READ_REQ_sum'], 1.0):12.4f}")
+        if "GRBM_UTCL2_BUSY" in c and "GRBM_GUI_ACTIVE" in c:
+            print(f"UTCL2 busy fraction (GRBM_UTCL2_BUSY / GUI)   {c['GRBM_UTCL2_BUSY'] / c['GRBM_GUI_ACTIVE']:12.3f}")
+        if "GRBM_GUI_ACTIVE" in c:
+            cyc = c["GRBM_GUI_ACTIVE"] / xcd
+            for k in ("TCP_UTCL1_STALL_MULTI_MISS_sum", "TCP_UTCL1_SERIALIZATION_STALL_sum", "TCP_UTCL1_STALL_LFIFO_NO_RES_sum",
+                      "TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum", "TCP_PENDING_STALL_CYCLES_sum"):
+                if k in c:
+                    print(f"{k:40s} per CU per cycle {c[k] / cus / cyc:8.4f}")
     if "SQ_WAVE_CYCLES" in c:
         for k in ("SQ_BUSY_CYCLES", "SQ_WAIT_INST_ANY", "SQ_VMEM_TA_ADDR_FIFO_FULL", "SQ_VMEM_TA_CMD_FIFO_FULL",
                   "SQ_ACTIVE_INST_VMEM", "SQ_ACTIVE_INST_VALU"):
