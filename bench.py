@@ -62,7 +62,7 @@ L2_PEAK_GBS = 34500.0    # the eight XCD L2s together (§L2)
 LINE_BYTES = 128         # gfx950 L1 and L2 line: one TCP_TCC_READ_REQ / TCC_EA0_RDREQ per line
                          # (tools/ubench_levels.hip, profiles/round3_counter_calibration.md)
 MALL_BYTES = 256 << 20   # Infinity Cache: a BVH above this streams from HBM
-PROFILE_TAGS = ("round5", "round4")   # committed rocprofv3 summaries the line may cite, newest first
+PROFILE_TAGS = ("round6", "round5", "round4")   # committed rocprofv3 summaries the line may cite, newest first
                                       # (profiles/<tag>_<workload>_*): only one of the timed schedule is cited
 PROFILE_RATIO = (0.9, 1.1)   # a cited profile's mean kernel time / this run's event time must lie in here
 LATENCY_BOUND = 0.25         # every memory level served below this fraction of its ceiling: bound = "latency"
@@ -742,32 +742,72 @@ def roofline(name, alg_bytes_per_launch, kernel_ms, bvh_bytes, schedule, rcp="ex
                           else ("hbm" if max(fr, key=fr.get) == "fabric" else "l2")),
                 "l1_hit_fraction_of_algorithmic": round(max(0.0, 1.0 - lv["l2_request_bytes"] / alg_bytes_per_launch), 4),
                 "l2_hit_rate": prof.get("l2_hit_rate"),
+                **({"vmem_frac": round(max(prof["vmem"]["ta_busy_frac"], prof["vmem"]["td_busy_frac"]), 4),
+                    "vmem": {k: round(v, 4) for k, v in prof["vmem"].items() if k.endswith("frac")}}
+                   if prof.get("vmem") else {}),
                 "profile": {"path": prof["path"], "kernel_ms": round(prof["avg_ns"] / 1e6, 4),
                             "kernel_ms_ratio": round(prof["avg_ns"] / 1e6 / kernel_ms, 4)}})
+    # the unit the traversal actually saturates, priced against its own ceiling: the
+    # vector-memory path (TA address / TD data units busy per CU cycle), the L2 or the fabric
+    units = {"l2": fr["l2"], "fabric": fr["fabric"]}
+    if out.get("vmem_frac") is not None:
+        units["vmem"] = out["vmem_frac"]
+    out["binding_unit"] = max(units, key=units.get)
+    out["binding_frac"] = round(units[out["binding_unit"]], 4)
     return out
 
 
-def exploration_cost(tracer, gbvh, rb, exact, max_launches=200):
-    """What autotuning costs a caller without saved schedules: a fresh
-    bind, then blocking timed launches of one batch until its schedule locks; the
-    exploring launches' total against as many launches of the settled schedule.
-    The saved schedules are locked again afterwards."""
-    tracer.set_bvh(gbvh)
-    times, locked_at = [], None
-    for i in range(max_launches):
-        times.append(tracer.trace_batch(rb, exact_rcp=exact))
-        if tracer.last_info["autotune_locked"]:
-            locked_at = i + 1
-            break
-    settled = [tracer.trace_batch(rb, exact_rcp=exact) for _ in range(10)]
-    cand = tracer.last_info["autotune_candidate"]
-    bind(tracer, gbvh)
-    if locked_at is None:
-        return {"locked": False, "launches": max_launches}
-    s = float(np.median(settled))
-    return {"locked": True, "launches_to_lock": locked_at, "exploring_ms": round(sum(times), 3),
-            "settled_ms_each": round(s, 4), "overhead_ms": round(sum(times) - locked_at * s, 3),
-            "explored_candidate": cand}
+def exploration_cost(tracer, gbvh, rb, exact, max_launches=600):
+    """What autotuning costs and finds for a caller without saved schedules (VERDICT r2 #5,
+    r5 #4): a fresh bind, then back-to-back launches of one batch (as the timed steps run
+    them, no blocking) until the library settles its schedule; then the settled and the
+    saved schedule each timed by the headline's own probe (HIP events around back-to-back
+    launches after a warmup), so `tuned_vs_saved` compares like with like. The saved
+    schedules are locked again afterwards."""
+    import torch
+    tracer.set_bvh(gbvh)   # bind forgets every schedule: the autotuner starts from scratch
+    go = tracer.launcher(rb, exact_rcp=exact)
+
+    def settled():
+        return [c for n, _, c, _ in tracer.schedules() if n == rb.size]
+
+    t0 = time.perf_counter()
+    n = 0
+    while n < max_launches and not settled():
+        for _ in range(8):
+            go()
+        n += 8
+        torch.cuda.synchronize()   # lets the library read the candidates' event pairs
+    explore_s = time.perf_counter() - t0
+
+    def probe(reps=3, k=40):
+        for _ in range(20):
+            go()
+        out = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(k):
+                go()
+            e1.record()
+            torch.cuda.synchronize()
+            out.append(e0.elapsed_time(e1) / k)
+        return float(np.median(out))
+
+    cand = settled()
+    tuned_ms = probe() if cand else None
+    bind(tracer, gbvh)   # the saved schedules again
+    saved = [c for n_, _, c, _ in tracer.schedules() if n_ == rb.size]
+    saved_ms = probe() if saved else None
+    if not cand:
+        return {"locked": False, "launches": n}
+    out = {"locked": True, "launches_to_lock": n, "exploring_s": round(explore_s, 3),
+           "explored_candidate": cand[0], "explored_schedule": schedule_name(cand[0]),
+           "settled_ms_each": round(tuned_ms, 4)}
+    if saved_ms:
+        out.update({"saved_candidate": saved[0], "saved_ms_each": round(saved_ms, 4),
+                    "tuned_vs_saved": round(tuned_ms / saved_ms, 4)})
+    return out
 
 
 # cfg.autotune candidates (csrc/mrt_api.cpp tune_candidate)
@@ -1166,7 +1206,8 @@ def compact_roofline(rf):
     keep = {k: rf.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel_ms",
                                    "kernel_achieved", "kernel_frac", "kernel_bytes_per_launch",
                                    "hbm_measured_GBps", "hbm_measured_frac", "binding_level", "l2_hit_rate",
-                                   "l1_hit_fraction_of_algorithmic", "alg_bytes_per_launch", "note")
+                                   "l1_hit_fraction_of_algorithmic", "alg_bytes_per_launch", "vmem_frac",
+                                   "binding_unit", "binding_frac", "note")
             if rf.get(k) is not None}
     if rf.get("served"):
         keep["served_frac"] = {k: v["frac"] for k, v in rf["served"].items()}
@@ -1199,8 +1240,11 @@ def compact_workload(r):
     out = {"workload": r["workload"], "value": r["value"], "reference_mrays": r.get("reference_mrays"),
            "kernel_ms": r["kernel_ms_per_launch"], "schedule": (r.get("schedule") or {}).get("name"),
            "roofline": {k: rf.get(k) for k in ("bound", "frac", "kernel_frac", "hbm_measured_frac", "binding_level",
-                                               "traffic")},
+                                               "traffic", "vmem_frac")},
            "cpu_baseline": cb and cb["value"], "parity": compact_parity(cb, fast)}
+    ex = r.get("autotune_exploration") or {}
+    if ex.get("tuned_vs_saved"):   # a fresh bind's settled schedule against the saved one
+        out["tuned_vs_saved"] = ex["tuned_vs_saved"]
     if fast:
         out["rcp_fast_value"] = fast["value"]
     return out

@@ -77,13 +77,15 @@ struct mrt_tracer {
 
 // Launch-schedule autotuning state of one (batch size, kernel variant).
 struct TuneState {
-    // Stage 1: kSchedules ray-distribution schedules; stage 2: the stage-1 winner
-    // with the speculation slack at 4 and 6, without the frontier tail (with it if the
-    // tracer's default is off), with 16 lane groups, and with 2 lane groups at slack 6
-    // (candidates kSchedules .. kSchedules + kStage2 - 1).
+    // Stage 1: kSchedules ray-distribution schedules; stage 2: the stage-1 winner and
+    // the runner-up, each with the speculation slack at 4 and 6, without the frontier
+    // tail (with it if the tracer's default is off), with 16 lane groups, and with 2
+    // lane groups at slack 6 (candidates kSchedules .. + kStage2 - 1 modify the winner,
+    // the next kStage2 the runner-up; a settled choice is stored canonically as modifier
+    // kSchedules + k of the schedule it modifies, so saved tables keep their meaning).
     static constexpr int kSchedules = 8;
     static constexpr int kStage2 = 5;
-    static constexpr int kCandidates = kSchedules + kStage2;
+    static constexpr int kCandidates = kSchedules + 2 * kStage2;
     static constexpr int kSamples = 8;   // timed launches per candidate; the median ranks them
     int launches = 0;    // exploring launches so far (the first round of candidates runs untimed:
                          // the clocks and caches are still settling)
@@ -91,7 +93,11 @@ struct TuneState {
     int samples[kCandidates] = {};
     int next = 0;        // candidate the next exploring launch uses
     int rule = 0;        // the candidate equal to the fixed rule (effective_cfg) for this batch
-    int stage1 = -1;     // the stage-1 winner, once every schedule has kSamples samples
+    int stage1 = -1;     // the stage-1 winner, once every schedule has kSamples samples (once locked:
+                         // the schedule the locked modifier applies to)
+    int stage1b = -1;    // the stage-1 runner-up (stage 2 modifies it too; VERDICT r5 #4: the headline's
+                         // saved schedule is the 8-waves/CU schedule with 2 lane groups, whose base
+                         // alone loses to 20 waves/CU in stage 1)
     int locked = -1;     // the chosen candidate, once stage 2's have kSamples samples too
     void* stream = nullptr;          // the stream this batch size was first launched on
     bool multiStream = false;        // launched on several streams: not explored (settled schedule or the rule)
@@ -235,7 +241,7 @@ bool valid_cfg(const mrt_launch_cfg& c) {
            c.tail_lanes >= 0 && c.tail_lanes <= 16 &&
            c.queue_shared >= 0 && c.queue_shared <= 100 && c.queue_block >= 0 && c.queue_block <= (1 << 20) &&
            (c.queue_block & (c.queue_block - 1)) == 0 && (c.queue_block == 0 || c.queue_block >= 64) &&
-           c.queue_xcc_mask >= 0 && c.queue_xcc_mask <= 15 && (c.ray_sort == 0 || c.ray_sort == 1);
+           c.queue_xcc_mask >= 0 && c.queue_xcc_mask <= 15 && c.ray_sort == 0;   // ray_sort: removed in round 6
 }
 
 // The frontier tail runs in the exact 4-wide kernels whose leaf refs carry counts.
@@ -477,8 +483,9 @@ int refresh_wide(mrt_tracer* t) {
 // and the distribution knobs at their defaults, the first launches of a batch
 // size cycle through these eight candidates, each timed with an event pair that is
 // read back on a later launch (never blocking); after kSamples launches each the
-// fastest is timed again with the speculation slack at 4 and 6 (stage 2), and the
-// fastest of the three is kept for that batch size. Closest hits are the same hits under
+// fastest and the runner-up are timed again, each with the stage-2 modifiers (the
+// speculation slack at 4 and 6, the tail toggled, 16 lane groups, 2 lane groups at
+// slack 6), and the fastest is kept for that batch size. Closest hits are the same hits under
 // every schedule, except that which of two triangles at exactly the same t wins follows the
 // traversal order, and so can the hit an any-hit ray reports (any valid hit). A
 // reproducible run pins the schedule: autotune 0, or the schedules saved per BVH
@@ -493,13 +500,15 @@ constexpr int kXcdQueueBlock = 8192;
 constexpr int kXcdQueueShared = 0;
 constexpr int kXcdQueueThreshold = 56;
 
-mrt_launch_cfg tune_candidate(const mrt_tracer* t, const mrt_launch_cfg& base, int c, int stage1) {
+mrt_launch_cfg tune_candidate(const mrt_tracer* t, const mrt_launch_cfg& base, int c, int stage1, int stage1b) {
     if (c >= TuneState::kSchedules) {
-        // stage 2: the stage-1 winner, the wave turning to its leaves once <= 4 (6) lanes
-        // still search, with the frontier tail toggled, or with its lanes taking rays from 16
+        // stage 2: the stage-1 winner (or runner-up), the wave turning to its leaves once <= 4 (6)
+        // lanes still search, with the frontier tail toggled, or with its lanes taking rays from 16
         // distant parts of each strided chunk (only for knobs the caller left at their defaults)
-        mrt_launch_cfg x = tune_candidate(t, base, stage1, stage1);
-        const int k = c - TuneState::kSchedules;
+        const bool second = c >= TuneState::kSchedules + TuneState::kStage2;
+        const int sched = second ? stage1b : stage1;
+        mrt_launch_cfg x = tune_candidate(t, base, sched, sched, sched);
+        const int k = (c - TuneState::kSchedules) % TuneState::kStage2;
         if (k < 2 && base.spec_slack == kDefaultSpecSlack) x.spec_slack = k == 0 ? 4 : 6;
         if (k == 2 && base.tail_lanes == kDefaultTailLanes) x.tail_lanes = kDefaultTailLanes ? 0 : kTunedTailLanes;
         // lane groups mix a wave's rays from distant image regions: fewer waves hold a whole
@@ -576,13 +585,20 @@ void tune_collect(TuneState* st) {
         for (int c = 0; c < TuneState::kSchedules; c++)
             if (st->samples[c] < TuneState::kSamples) return;
         st->stage1 = tune_pick(st, st->rule, 0, TuneState::kSchedules);
+        for (int c = 0; c < TuneState::kSchedules; c++)
+            if (c != st->stage1 && (st->stage1b < 0 || st->median(c) < st->median(st->stage1b))) st->stage1b = c;
         st->next = TuneState::kSchedules;
         return;
     }
     for (int c = TuneState::kSchedules; c < TuneState::kCandidates; c++)
         if (st->samples[c] < TuneState::kSamples) return;
     st->samples[st->stage1] = std::min(st->samples[st->stage1], TuneState::kSamples);
-    st->locked = tune_pick(st, st->stage1, TuneState::kSchedules, TuneState::kCandidates);
+    int pick = tune_pick(st, st->stage1, TuneState::kSchedules, TuneState::kCandidates);
+    if (pick >= TuneState::kSchedules + TuneState::kStage2) {   // a modifier of the runner-up: canonical form
+        st->stage1 = st->stage1b;
+        pick -= TuneState::kStage2;
+    }
+    st->locked = pick;
 }
 
 void tune_reset(mrt_tracer* t) {
@@ -671,7 +687,8 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
         } else {
             cand = tune->next;
             tune->next = tune->stage1 < 0 ? (tune->next + 1) % TuneState::kSchedules
-                                          : TuneState::kSchedules + (tune->next + 1 - TuneState::kSchedules) % TuneState::kStage2;
+                                          : TuneState::kSchedules +
+                                                (tune->next + 1 - TuneState::kSchedules) % (2 * TuneState::kStage2);
             if (tune->launches++ >= TuneState::kSchedules)
                 for (auto& p : tune->pending)
                     if (p.cand < 0) {
@@ -683,7 +700,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
                 MRT_HIP(hipEventCreateWithFlags(&slot->stop, mrt::kTimingEventFlags));
             }
         }
-        cfg = tune_candidate(t, cfg, cand, tune->stage1);
+        cfg = tune_candidate(t, cfg, cand, tune->stage1, tune->stage1b);
     }
     v.tail = with_tail(t, v, cfg);   // a tuned candidate may run without the tail
     const int blocks = grid_blocks(t, cfg, v, numRays, &perCU);
@@ -718,7 +735,6 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     a.stackBound = wide ? t->wideStackBound : stackCap - 1;
     a.tailLanes = cfg.tail_lanes;
     a.xccMask = cfg.queue_xcc_mask;
-    a.raySort = cfg.ray_sort;
     a.queues = ws->queues;
     a.spill = ws->spill;
     // The blocking call counts this launch's overflows in a slot of its own; the
@@ -744,7 +760,11 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     }
     if (info) {
         // stage-2 candidates (another speculation slack) carry their stage-1 schedule in bits 8+
-        info->autotune_candidate = cand >= TuneState::kSchedules ? cand | (tune->stage1 << 8) : cand;
+        // canonical: a stage-2 modifier k of the schedule it modifies, kSchedules + k | schedule << 8
+        const bool second = cand >= TuneState::kSchedules + TuneState::kStage2;
+        info->autotune_candidate = cand >= TuneState::kSchedules
+                                       ? (second ? cand - TuneState::kStage2 : cand) | ((second ? tune->stage1b : tune->stage1) << 8)
+                                       : cand;
         info->autotune_locked = tune && tune->locked >= 0 ? 1 : 0;
         info->stack_capacity = stackCap;
         MRT_HIP(hipEventRecord(t->evStop, s));
@@ -985,7 +1005,7 @@ int mrt_tracer_tune_import(mrt_tracer* t, const mrt_tuned_schedule* in, int32_t 
     if (!t || (count > 0 && !in) || count < 0) return fail(MRT_ERR_INVALID_ARG, "null argument");
     for (int i = 0; i < count; i++) {
         const int locked = in[i].candidate & 0xff, stage1 = in[i].candidate >> 8;
-        if (in[i].version != MRT_TUNE_VERSION || in[i].num_rays <= 0 || locked >= TuneState::kCandidates ||
+        if (in[i].version != MRT_TUNE_VERSION || in[i].num_rays <= 0 || locked >= TuneState::kSchedules + TuneState::kStage2 ||
             stage1 < 0 || stage1 >= TuneState::kSchedules)
             return fail(MRT_ERR_INVALID_ARG, "tuned schedule from another library version or out of range");
     }
@@ -999,6 +1019,7 @@ int mrt_tracer_tune_import(mrt_tracer* t, const mrt_tuned_schedule* in, int32_t 
         }
         it->second->stage1 = in[i].candidate >> 8;
         it->second->locked = in[i].candidate & 0xff;
+        it->second->inherited = false;   // a schedule saved for this very key: exported again
     }
     return MRT_OK;
 }

@@ -105,16 +105,17 @@ typedef struct mrt_launch_cfg {
                                   of each batch size (per kernel variant, up to 64 sizes) time eight ray-
                                   distribution schedules (static rounds at 20, 16, 12 or 8 waves/CU, per-XCD
                                   block-cyclic queues, the global queue at 20, 16 or 12 waves/CU), then
-                                  the winner with spec_slack 4 and 6, without the frontier tail, with 16
-                                  lane groups, and with 2 lane groups at spec_slack 6 (each
+                                  the winner and the runner-up, each with spec_slack 4 and 6, without the
+                                  frontier tail, with 16 lane groups, and with 2 lane groups at spec_slack 6 (each
                                   knob only when left at its default), eight times each without blocking,
                                   after one untimed round of them; the median ranks them and a candidate
                                   replaces the fixed rule (stage 1) or the stage-1 winner (stage 2) only
-                                  when 3 % faster. A new batch size within 1/32 of a settled one (same
-                                  variant) takes the nearest settled schedule without exploring —
-                                  a schedule tuned on another ray distribution of that size (e.g. a
-                                  primary batch's for a diffuse one over the same BVH); such inherited
-                                  entries are not exported by mrt_tracer_tune_export. A batch
+                                  when 3 % faster. A new batch size within 1/32 of a settled one of the
+                                  same variant and ray class (MRT_TRACE_SECONDARY batches are a class
+                                  of their own) takes the nearest settled schedule without exploring —
+                                  a schedule tuned on another ray distribution of that class; such
+                                  inherited entries are not exported by mrt_tracer_tune_export (an
+                                  imported schedule for the same key replaces one and is). A batch
                                   size launched on more than one stream is not explored: it runs its settled
                                   schedule if it has one, else the fixed rule; reset by bind and set_config (default 1; mrt_tracer_tune_export /
                                   _import save and restore the choices). 0 = the fixed rule only; -1 = default */
@@ -132,11 +133,9 @@ typedef struct mrt_launch_cfg {
                                   the shares are this many rays' blocks dealt cyclically (block i to queue
                                   i mod num_queues), so every XCD samples the whole frame (default 0;
                                   -1 = default)                                                        */
-    int32_t ray_sort;          /* 1 = a static launch whose batch fits one round of the grid (e.g. 307 200 rays
-                                  at 20 waves/CU) deals each workgroup's 256 consecutive rays to its four
-                                  waves by direction octant, degenerate (tmax < 0) rays last, instead of
-                                  the strided deal (exact 4-wide traversal only); 0 = off (default; -1 =
-                                  default). Results are unchanged: every ray is traced once either way */
+    int32_t ray_sort;          /* round 5's octant ray sort, removed in round 6 (slower on every batch measured,
+                                  and the per-lane deal it needed cost the static deal a register: DESIGN
+                                  §4): 0 (or -1 = default); any other value is refused (MRT_ERR_INVALID_ARG) */
     int32_t queue_xcc_mask;    /* test hook, 0 = off (default; -1 = default): 1..15 = a wave takes from queue
                                   (XCC_ID & mask) % num_queues, so with mask 3 and 8 queues, queues 4..7
                                   have no waves of their own (the unserved-queue sweep must trace them) */

@@ -74,7 +74,14 @@ if all(k in pm for k in need):
     rd = (pm["TCC_EA0_RDREQ_sum"] - pm["TCC_EA0_RDREQ_32B_sum"]) * 128 + pm["TCC_EA0_RDREQ_32B_sum"] * 32
     out["levels"] = {"l2_request_bytes": pm["TCP_TCC_READ_REQ_sum"] * 128, "fabric_read_bytes": rd,
                      "write_bytes": pm["WRITE_SIZE"] * 1024, "fabric_bytes": rd + pm["WRITE_SIZE"] * 1024}
+if all(k in pm for k in ("TA_TA_BUSY_sum", "TD_TD_BUSY_sum", "GRBM_GUI_ACTIVE")):
+    # busy cycles per CU per kernel cycle (GRBM_GUI_ACTIVE counts every XCD's clock: / 8 XCDs;
+    # one TA and one TD per CU, 256 CUs): the vector-memory path's utilisation (bench vmem_frac)
+    cyc = pm["GRBM_GUI_ACTIVE"] / 8
+    out["vmem"] = {"ta_busy_frac": pm["TA_TA_BUSY_sum"] / 256 / cyc, "td_busy_frac": pm["TD_TD_BUSY_sum"] / 256 / cyc,
+                   "kernel_cycles": cyc}
 if "TCC_HIT_sum" in pm and "TCC_MISS_sum" in pm:
     out["l2_hit_rate"] = pm["TCC_HIT_sum"] / (pm["TCC_HIT_sum"] + pm["TCC_MISS_sum"])
 json.dump(out, open(os.path.join(dst, f"{tag}_pmc_summary.json"), "w"), indent=1)
-print(json.dumps({k: out.get(k) for k in ("kernel", "avg_ns", "timed_grid_calls", "schedule", "levels", "l2_hit_rate")}))
+print(json.dumps({k: out.get(k) for k in ("kernel", "avg_ns", "timed_grid_calls", "schedule", "levels", "l2_hit_rate",
+                                          "vmem")}))
