@@ -241,7 +241,7 @@ bool valid_cfg(const mrt_launch_cfg& c) {
            c.tail_lanes >= 0 && c.tail_lanes <= 16 &&
            c.queue_shared >= 0 && c.queue_shared <= 100 && c.queue_block >= 0 && c.queue_block <= (1 << 20) &&
            (c.queue_block & (c.queue_block - 1)) == 0 && (c.queue_block == 0 || c.queue_block >= 64) &&
-           c.queue_xcc_mask >= 0 && c.queue_xcc_mask <= 15 && c.ray_sort == 0;   // ray_sort: removed in round 6
+           c.queue_xcc_mask >= 0 && c.queue_xcc_mask <= 15 && (c.ray_sort == 0 || c.ray_sort == 1);
 }
 
 // The frontier tail runs in the exact 4-wide kernels whose leaf refs carry counts.
@@ -735,6 +735,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     a.stackBound = wide ? t->wideStackBound : stackCap - 1;
     a.tailLanes = cfg.tail_lanes;
     a.xccMask = cfg.queue_xcc_mask;
+    a.raySort = cfg.ray_sort;
     a.queues = ws->queues;
     a.spill = ws->spill;
     // The blocking call counts this launch's overflows in a slot of its own; the

@@ -55,6 +55,8 @@ struct TraceArgs {
                                // keeps this much headroom before it expands more than one entry per step
     int tailLanes;            // exact 4-wide speculative kernels: a wave that cannot refill and is down to
                                // this many live lanes finishes them in the frontier tail (0 = off)
+    int raySort;               // cfg.ray_sort: a one-round static launch deals each workgroup's 256-ray tile
+                               // to its waves by direction octant (exact 4-wide kernels)
     int xccMask;               // test hook (cfg.queue_xcc_mask): > 0 = a wave's queue is (XCC_ID & mask) %
                                // numQueues, so the queues above mask have no waves of their own
     unsigned* queues;          // numQueues heads, kQueueStrideWords apart, zeroed per launch

@@ -133,9 +133,11 @@ typedef struct mrt_launch_cfg {
                                   the shares are this many rays' blocks dealt cyclically (block i to queue
                                   i mod num_queues), so every XCD samples the whole frame (default 0;
                                   -1 = default)                                                        */
-    int32_t ray_sort;          /* round 5's octant ray sort, removed in round 6 (slower on every batch measured,
-                                  and the per-lane deal it needed cost the static deal a register: DESIGN
-                                  §4): 0 (or -1 = default); any other value is refused (MRT_ERR_INVALID_ARG) */
+    int32_t ray_sort;          /* 1 = a static launch whose batch fits one round of the grid (e.g. 307 200 rays
+                                  at 20 waves/CU) deals each workgroup's 256 consecutive rays to its four
+                                  waves by direction octant, degenerate (tmax < 0) rays last, instead of
+                                  the strided deal (exact 4-wide traversal only); 0 = off (default; -1 =
+                                  default). Results are unchanged: every ray is traced once either way */
     int32_t queue_xcc_mask;    /* test hook, 0 = off (default; -1 = default): 1..15 = a wave takes from queue
                                   (XCC_ID & mask) % num_queues, so with mask 3 and 8 queues, queues 4..7
                                   have no waves of their own (the unserved-queue sweep must trace them) */

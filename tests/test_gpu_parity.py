@@ -220,6 +220,8 @@ def test_exact_reciprocal_is_correctly_rounded_for_every_float(tracer):
                                  dict(num_queues=5, queue_shared=5, queue_block=1024, fetch_threshold=40, waves_per_cu=4),
                                  dict(num_queues=8, queue_block=8192, fetch_threshold=56, waves_per_cu=20),
                                  dict(num_queues=8, queue_block=256, fetch_threshold=56, waves_per_cu=4),
+                                 dict(ray_sort=1), dict(ray_sort=1, tail_lanes=0), dict(ray_sort=1, waves_per_cu=4),
+                                 dict(ray_sort=1, lane_groups=16), dict(ray_sort=1, waves_per_cu=8, lds_stack=8),
                                  dict(lane_groups=2, waves_per_cu=8), dict(lane_groups=64, tail_lanes=0),
                                  dict(lane_groups=4, waves_per_cu=4), dict(lane_groups=16, waves_per_cu=8, lds_stack=8)],
                          ids=lambda c: ",".join(f"{k}={v}" for k, v in c.items()))
@@ -265,8 +267,7 @@ def test_queues_without_waves_are_still_traced(tracer, cfg):
                          ids=lambda w: "-".join(map(str, w)))
 @pytest.mark.parametrize("waves,groups", [(20, 1), (8, 1), (8, 2), (16, 16)])
 def test_static_deal_traces_every_ray_once(tracer, wl, waves, groups):
-    """The static strided deal (round 6: each wave's slot in its XCD group is wave-uniform, a
-    lane's place = slot * 64 + lane) over one round (20 waves/CU: 307 200 rays) and several
+    """The static strided deal over one round (20 waves/CU: 307 200 rays) and several
     (8 waves/CU), with lane groups: every ray traced exactly once and equal to the oracle —
     closest hits bit-identical, any hits genuine (hit/miss identical)."""
     bufs, rays, any_hit, want, _ = scene_setup(*wl)
@@ -282,15 +283,24 @@ def test_static_deal_traces_every_ray_once(tracer, wl, waves, groups):
         tracer.set_config(**saved)
 
 
-def test_ray_sort_is_refused(tracer):
-    """cfg.ray_sort (round 5's octant ray sort) was removed in round 6: a 1 is refused, 0 and -1 accepted."""
-    from mrt import _lib
+@pytest.mark.parametrize("wl", [("conference", 640, 480, "ao"), ("mori", 640, 480, "ao"), ("sponza", 640, 480, "diffuse"),
+                                ("hairball:800", 640, 480, "diffuse"), ("bunny", 640, 480, "primary")],
+                         ids=lambda w: "-".join(map(str, w)))
+@pytest.mark.parametrize("waves", [20, 8])
+def test_ray_sort_traces_every_ray_once(tracer, wl, waves):
+    """cfg.ray_sort: a one-round static launch deals each workgroup's 256-ray tile by direction
+    octant (degenerate rays last). Every ray is traced exactly once and equals the oracle:
+    closest hits bit-identical, any hits genuine (hit/miss identical). At 8 waves/CU the
+    307 200-ray batch needs several rounds, so the sort is skipped there (the same results)."""
+    bufs, rays, any_hit, want, _ = scene_setup(*wl)
     saved = tracer.config()
     try:
-        with pytest.raises(_lib.MrtError):
-            tracer.set_config(ray_sort=1)
-        tracer.set_config(ray_sort=0)
-        tracer.set_config(ray_sort=-1)
+        tracer.set_config(ray_sort=1, waves_per_cu=waves, autotune=0)
+        res, _ = gpu_trace(tracer, bufs, rays, any_hit, exact=True, spec=True)
+        if any_hit:
+            assert_valid_hits(rays, res, want, bufs)
+        else:
+            assert np.array_equal(res[:, :2], want[:, :2])
     finally:
         tracer.set_config(**saved)
 

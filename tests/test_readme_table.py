@@ -46,3 +46,24 @@ def test_committed_round5_table_is_complete():
             assert r["parity_same"] + r["exact_t_ties"] == r["parity_rays"]
             if r["workload"] != "san-diffuse-640x480":
                 assert r["exact_t_ties"] == 0
+
+
+def test_committed_round6_table_runs_the_shipped_schedules():
+    """the README table must report what a user of the shipped schedule table
+    gets — every row's saved schedules (fingerprint, batch size, variant -> candidate) equal the
+    package's mrt/tuned_schedules.json entries, so no cell depends on a per-cell lock."""
+    import pytest
+    path = os.path.join(REPO, "profiles", "round6_readme_table.json")
+    if not os.path.exists(path):
+        pytest.skip("no round-6 table")
+    with open(path) as f:
+        rows = json.load(f)
+    with open(os.path.join(REPO, "gpu-ray-tracing_amd", "mrt", "tuned_schedules.json")) as f:
+        shipped = json.load(f)
+    assert {r["workload"] for r in rows} == {c[0] for c in rt.CELLS}
+    for r in rows:
+        table = {(n, v): c for n, v, c, _ in shipped["bvhs"][r["fingerprint"]]}
+        assert r["schedules"], r["workload"]
+        for n, v, c in r["schedules"]:
+            assert table.get((n, v)) == c, (r["workload"], n, v, c, table.get((n, v)))
+        assert r["x_readme"] > 1 and r["parity_all_rays"]
