@@ -757,7 +757,7 @@ def roofline(name, alg_bytes_per_launch, kernel_ms, bvh_bytes, schedule, rcp="ex
     return out
 
 
-def exploration_cost(tracer, gbvh, rb, exact, max_launches=600):
+def exploration_cost(tracer, gbvh, rb, exact, max_launches=1200):
     """What autotuning costs and finds for a caller without saved schedules (VERDICT r2 #5,
     r5 #4): a fresh bind, then back-to-back launches of one batch (as the timed steps run
     them, no blocking) until the library settles its schedule; then the settled and the
@@ -829,7 +829,7 @@ def schedule_name(c):
     if (c & 0xff) >= 8:
         return f"{SCHEDULES[c >> 8]}, " + {8: "spec_slack 4", 9: "spec_slack 6", 10: "no frontier tail", 11: "16 lane groups",
                                             12: "2 lane groups, spec_slack 6"}[c & 0xff]
-    return SCHEDULES[c]
+    return SCHEDULES[c & 0xff]   # (an exported stage-1 choice carries its own number in the stage-1 byte)
 
 
 def schedule_of(tracer, rb, exact):

@@ -83,12 +83,22 @@ struct TuneState {
     // lane groups at slack 6 (candidates kSchedules .. + kStage2 - 1 modify the winner,
     // the next kStage2 the runner-up; a settled choice is stored canonically as modifier
     // kSchedules + k of the schedule it modifies, so saved tables keep their meaning).
+    // Stage 3: the stage-2 winner's modifier on each other schedule (kStage3 candidates from
+    // kStage3First): e.g. 16 lane groups paid off at 16 waves/CU though the two stage-1 leaders
+    // were 20 and 12 waves/CU (bunny primary 640x480).
     static constexpr int kSchedules = 8;
     static constexpr int kStage2 = 5;
-    static constexpr int kCandidates = kSchedules + 2 * kStage2;
+    static constexpr int kStage3First = kSchedules + 2 * kStage2;
+    static constexpr int kStage3 = kSchedules - 2;
+    static constexpr int kCandidates = kStage3First + kStage3;
     static constexpr int kSamples = 8;   // timed launches per candidate; the median ranks them
+    // A candidate runs kRun consecutive launches at a time, the first untimed: a launch right
+    // after another schedule's inherits its cache and queue state (round 6: one launch per
+    // candidate ranked a 42-us batch's schedules 3.5 % off their steady-state order).
+    static constexpr int kRun = 4;
     int launches = 0;    // exploring launches so far (the first round of candidates runs untimed:
                          // the clocks and caches are still settling)
+    int runPos = 0;      // position of the next launch in its candidate's run
     float times[kCandidates][kSamples];
     int samples[kCandidates] = {};
     int next = 0;        // candidate the next exploring launch uses
@@ -98,7 +108,10 @@ struct TuneState {
     int stage1b = -1;    // the stage-1 runner-up (stage 2 modifies it too; VERDICT r5 #4: the headline's
                          // saved schedule is the 8-waves/CU schedule with 2 lane groups, whose base
                          // alone loses to 20 waves/CU in stage 1)
-    int locked = -1;     // the chosen candidate, once stage 2's have kSamples samples too
+    int stage2 = -1;     // the stage-2 pick (a modifier of stage1 or stage1b), once stage 2's have kSamples
+    int s3mod = -1;      // its modifier k, tried on the schedules in s3sched (stage 3)
+    int s3sched[kStage3] = {};
+    int locked = -1;     // the chosen candidate (canonical: kSchedules + k of stage1), once settled
     void* stream = nullptr;          // the stream this batch size was first launched on
     bool multiStream = false;        // launched on several streams: not explored (settled schedule or the rule)
     bool inherited = false;          // took a nearby batch size's schedule (kTuneInherit): not exported
@@ -500,15 +513,31 @@ constexpr int kXcdQueueBlock = 8192;
 constexpr int kXcdQueueShared = 0;
 constexpr int kXcdQueueThreshold = 56;
 
-mrt_launch_cfg tune_candidate(const mrt_tracer* t, const mrt_launch_cfg& base, int c, int stage1, int stage1b) {
-    if (c >= TuneState::kSchedules) {
-        // stage 2: the stage-1 winner (or runner-up), the wave turning to its leaves once <= 4 (6)
+// The schedule and modifier (-1: none) of candidate c: stage 1 a schedule, stage 2 a modifier of
+// the stage-1 winner or runner-up, stage 3 the stage-2 modifier on another schedule. A settled
+// candidate is canonical: kSchedules + k modifies st->stage1.
+void tune_decode(const TuneState* st, int c, int* sched, int* mod) {
+    if (c < TuneState::kSchedules) {
+        *sched = c;
+        *mod = -1;
+    } else if (c < TuneState::kStage3First) {
+        const bool second = c >= TuneState::kSchedules + TuneState::kStage2;
+        *sched = second ? st->stage1b : st->stage1;
+        *mod = (c - TuneState::kSchedules) % TuneState::kStage2;
+    } else {
+        *sched = st->s3sched[c - TuneState::kStage3First];
+        *mod = st->s3mod;
+    }
+}
+
+mrt_launch_cfg tune_candidate(const mrt_tracer* t, const mrt_launch_cfg& base, int c, const TuneState* st) {
+    int sched = c, k = -1;
+    if (st) tune_decode(st, c, &sched, &k);
+    if (k >= 0) {
+        // stage 2/3: a schedule with the wave turning to its leaves once <= 4 (6)
         // lanes still search, with the frontier tail toggled, or with its lanes taking rays from 16
         // distant parts of each strided chunk (only for knobs the caller left at their defaults)
-        const bool second = c >= TuneState::kSchedules + TuneState::kStage2;
-        const int sched = second ? stage1b : stage1;
-        mrt_launch_cfg x = tune_candidate(t, base, sched, sched, sched);
-        const int k = (c - TuneState::kSchedules) % TuneState::kStage2;
+        mrt_launch_cfg x = tune_candidate(t, base, sched, nullptr);
         if (k < 2 && base.spec_slack == kDefaultSpecSlack) x.spec_slack = k == 0 ? 4 : 6;
         if (k == 2 && base.tail_lanes == kDefaultTailLanes) x.tail_lanes = kDefaultTailLanes ? 0 : kTunedTailLanes;
         // lane groups mix a wave's rays from distant image regions: fewer waves hold a whole
@@ -530,7 +559,7 @@ mrt_launch_cfg tune_candidate(const mrt_tracer* t, const mrt_launch_cfg& base, i
     x.num_queues = -1;
     x.queue_block = 0;
     x.queue_shared = 0;
-    switch (c) {
+    switch (sched) {
         case 0: break;                                                      // static rounds, 20 waves/CU
         case 1: x.waves_per_cu = 8; break;                                  // static rounds, fewer waves
         case 2:   // per-XCD queues of 8192-ray blocks dealt cyclically (every XCD samples the whole frame,
@@ -581,24 +610,44 @@ void tune_collect(TuneState* st) {
         p.cand = -1;
     }
     if (st->locked >= 0) return;
+    auto sampled = [&](int first, int last) {
+        for (int c = first; c < last; c++)
+            if (st->samples[c] < TuneState::kSamples) return false;
+        return true;
+    };
     if (st->stage1 < 0) {
-        for (int c = 0; c < TuneState::kSchedules; c++)
-            if (st->samples[c] < TuneState::kSamples) return;
+        if (!sampled(0, TuneState::kSchedules)) return;
         st->stage1 = tune_pick(st, st->rule, 0, TuneState::kSchedules);
         for (int c = 0; c < TuneState::kSchedules; c++)
             if (c != st->stage1 && (st->stage1b < 0 || st->median(c) < st->median(st->stage1b))) st->stage1b = c;
         st->next = TuneState::kSchedules;
+        st->runPos = 0;
         return;
     }
-    for (int c = TuneState::kSchedules; c < TuneState::kCandidates; c++)
-        if (st->samples[c] < TuneState::kSamples) return;
-    st->samples[st->stage1] = std::min(st->samples[st->stage1], TuneState::kSamples);
-    int pick = tune_pick(st, st->stage1, TuneState::kSchedules, TuneState::kCandidates);
-    if (pick >= TuneState::kSchedules + TuneState::kStage2) {   // a modifier of the runner-up: canonical form
-        st->stage1 = st->stage1b;
-        pick -= TuneState::kStage2;
+    if (st->stage2 < 0) {
+        if (!sampled(TuneState::kSchedules, TuneState::kStage3First)) return;
+        st->samples[st->stage1] = std::min(st->samples[st->stage1], TuneState::kSamples);
+        const int pick = tune_pick(st, st->stage1, TuneState::kSchedules, TuneState::kStage3First);
+        if (pick < TuneState::kSchedules) {   // no modifier beats the stage-1 winner: settled
+            st->locked = pick;
+            return;
+        }
+        int sched, mod;
+        tune_decode(st, pick, &sched, &mod);
+        st->stage2 = pick;
+        st->s3mod = mod;
+        for (int c = 0, i = 0; c < TuneState::kSchedules; c++)
+            if (c != st->stage1 && c != st->stage1b) st->s3sched[i++] = c;
+        st->next = TuneState::kStage3First;
+        st->runPos = 0;
+        return;
     }
-    st->locked = pick;
+    if (!sampled(TuneState::kStage3First, TuneState::kCandidates)) return;
+    const int pick = tune_pick(st, st->stage2, TuneState::kStage3First, TuneState::kCandidates);
+    int sched, mod;
+    tune_decode(st, pick, &sched, &mod);
+    st->stage1 = sched;   // canonical: modifier kSchedules + mod of schedule stage1
+    st->locked = TuneState::kSchedules + mod;
 }
 
 void tune_reset(mrt_tracer* t) {
@@ -685,11 +734,19 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
         if (tune->locked >= 0) {
             cand = tune->locked;
         } else {
+            // runs of kRun launches per candidate, cycling over the current stage's candidates;
+            // the first launch of a run (and the whole first cycle of stage 1) is untimed
             cand = tune->next;
-            tune->next = tune->stage1 < 0 ? (tune->next + 1) % TuneState::kSchedules
-                                          : TuneState::kSchedules +
-                                                (tune->next + 1 - TuneState::kSchedules) % (2 * TuneState::kStage2);
-            if (tune->launches++ >= TuneState::kSchedules)
+            const bool timed = tune->runPos > 0 && tune->launches >= TuneState::kSchedules * TuneState::kRun;
+            tune->launches++;
+            if (++tune->runPos == TuneState::kRun) {
+                tune->runPos = 0;
+                const int first = tune->stage1 < 0 ? 0 : (tune->stage2 < 0 ? TuneState::kSchedules : TuneState::kStage3First);
+                const int last = tune->stage1 < 0 ? TuneState::kSchedules
+                                                  : (tune->stage2 < 0 ? TuneState::kStage3First : TuneState::kCandidates);
+                tune->next = first + (tune->next + 1 - first) % (last - first);
+            }
+            if (timed)
                 for (auto& p : tune->pending)
                     if (p.cand < 0) {
                         slot = &p;
@@ -700,7 +757,7 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
                 MRT_HIP(hipEventCreateWithFlags(&slot->stop, mrt::kTimingEventFlags));
             }
         }
-        cfg = tune_candidate(t, cfg, cand, tune->stage1, tune->stage1b);
+        cfg = tune_candidate(t, cfg, cand, tune);
     }
     v.tail = with_tail(t, v, cfg);   // a tuned candidate may run without the tail
     const int blocks = grid_blocks(t, cfg, v, numRays, &perCU);
@@ -761,11 +818,10 @@ int trace_impl(mrt_tracer* t, const void* rays, void* results, int32_t numRays, 
     }
     if (info) {
         // stage-2 candidates (another speculation slack) carry their stage-1 schedule in bits 8+
-        // canonical: a stage-2 modifier k of the schedule it modifies, kSchedules + k | schedule << 8
-        const bool second = cand >= TuneState::kSchedules + TuneState::kStage2;
-        info->autotune_candidate = cand >= TuneState::kSchedules
-                                       ? (second ? cand - TuneState::kStage2 : cand) | ((second ? tune->stage1b : tune->stage1) << 8)
-                                       : cand;
+        // canonical: a modifier k of the schedule it modifies, kSchedules + k | schedule << 8
+        int sched = cand, mod = -1;
+        tune_decode(tune, cand, &sched, &mod);
+        info->autotune_candidate = mod >= 0 ? (TuneState::kSchedules + mod) | (sched << 8) : cand;
         info->autotune_locked = tune && tune->locked >= 0 ? 1 : 0;
         info->stack_capacity = stackCap;
         MRT_HIP(hipEventRecord(t->evStop, s));

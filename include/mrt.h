@@ -107,9 +107,11 @@ typedef struct mrt_launch_cfg {
                                   block-cyclic queues, the global queue at 20, 16 or 12 waves/CU), then
                                   the winner and the runner-up, each with spec_slack 4 and 6, without the
                                   frontier tail, with 16 lane groups, and with 2 lane groups at spec_slack 6 (each
-                                  knob only when left at its default), eight times each without blocking,
-                                  after one untimed round of them; the median ranks them and a candidate
-                                  replaces the fixed rule (stage 1) or the stage-1 winner (stage 2) only
+                                  knob only when left at its default), then the best such modifier on the
+                                  six other schedules (stage 3); each candidate runs four launches at a time
+                                  (the first untimed) until it has eight timed samples, without blocking,
+                                  after one untimed round; the median ranks them and a candidate
+                                  replaces the fixed rule (stage 1) or the previous stage's winner only
                                   when 3 % faster. A new batch size within 1/32 of a settled one of the
                                   same variant and ray class (MRT_TRACE_SECONDARY batches are a class
                                   of their own) takes the nearest settled schedule without exploring —

@@ -147,9 +147,10 @@ def test_automatic_launch_config(env, name, queues, waves):
 
 def test_autotuned_schedule_settles_and_keeps_results(env):
     """cfg.autotune (default): the first launches of a batch size cycle through eight
-    ray-distribution schedules, timed without blocking, then the winner with the
-    speculation slack at 4 and 6 and without the cooperative tail, and keep the
-    fastest by the median of eight samples. Every launch, exploring or settled,
+    ray-distribution schedules, timed without blocking in runs of four launches (the
+    first untimed), then the winner and the runner-up with each stage-2 modifier, then
+    the best modifier on the other schedules, and keep the fastest by the median of
+    eight samples. Every launch, exploring or settled,
     returns the oracle's closest hits; the settled choice exports and imports."""
     bench, scenes, tracer, threads = env
     name = "bunny-primary-1024x768"
@@ -161,7 +162,7 @@ def test_autotuned_schedule_settles_and_keeps_results(env):
     tracer.set_config(autotune=1)   # a fresh tuning state for this handle
     want, _, _ = O.trace(rb.rays.cpu().numpy(), *bufs, threads=threads)
     seen = set()
-    for i in range(200):
+    for i in range(600):
         tracer.trace_batch(rb, exact_rcp=True)   # blocking: every launch's timing is read back by the next
         seen.add(tracer.last_info["autotune_candidate"] & 0xff)
         got = rb.results_numpy()
@@ -194,7 +195,7 @@ def test_nearby_batch_sizes_and_other_streams_take_the_settled_schedule(env):
     tracer.set_config(autotune=1)   # a fresh tuning state
     n = rb.size
     ref = rb.view(0, n)
-    for _ in range(200):            # settle size n
+    for _ in range(600):            # settle size n
         tracer.trace_batch(ref, exact_rcp=True)
         if tracer.last_info["autotune_locked"]:
             break
@@ -234,14 +235,14 @@ def test_secondary_batches_keep_their_own_schedule(env):
     tracer.set_config(autotune=1)   # a fresh tuning state
     sec = RayBuffer(prim.rays.clone(), need_closest_hit=True, secondary=True)
     assert sec.view(0, 10).secondary and not prim.secondary
-    for _ in range(200):            # settle the primary class
+    for _ in range(600):            # settle the primary class
         tracer.trace_batch(prim, exact_rcp=True)
         if tracer.last_info["autotune_locked"]:
             break
     assert tracer.last_info["autotune_locked"] == 1
     tracer.trace_batch(sec, exact_rcp=True)   # same size and variant, the other class: it explores
     assert tracer.last_info["autotune_locked"] == 0
-    for _ in range(200):
+    for _ in range(600):
         tracer.trace_batch(sec, exact_rcp=True)
         if tracer.last_info["autotune_locked"]:
             break
