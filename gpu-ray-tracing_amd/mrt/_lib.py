@@ -54,7 +54,7 @@ class TunedSchedule(C.Structure):
     _fields_ = [("num_rays", i32), ("variant", i32), ("candidate", i32), ("version", i32)]
 
 
-MRT_TUNE_VERSION = 10
+MRT_TUNE_VERSION = 11
 
 
 class HostCamera(C.Structure):

@@ -76,7 +76,8 @@ class ScheduleStore:
     def save(self, path: str | None = None) -> None:
         path = path or self.path
         doc = {"version": _lib.MRT_TUNE_VERSION,
-               "note": "autotuner schedules per BVH fingerprint: [num_rays, variant, candidate, version]",
+               "note": "autotuner schedules per BVH fingerprint: [num_rays, variant, candidate, version]; "
+                       "variant | 512 = a batch of secondary rays (MRT_TRACE_SECONDARY)",
                "bvhs": {k: [list(e) for e in v] for k, v in sorted(self.table.items())}}
         tmp = f"{path}.{os.getpid()}.tmp"
         with open(tmp, "w") as f:

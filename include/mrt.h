@@ -191,7 +191,7 @@ typedef struct mrt_tuned_schedule {
     int32_t candidate;
     int32_t version;           /* MRT_TUNE_VERSION when exported; others are refused on import */
 } mrt_tuned_schedule;
-enum { MRT_TUNE_VERSION = 10 };
+enum { MRT_TUNE_VERSION = 11 };   /* 11: round 6 (schedules re-tuned on the round-6 library) */
 
 /* ---- handle API -------------------------------------------------------- */
 int  mrt_tracer_create(int device, mrt_tracer** out);

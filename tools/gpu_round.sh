@@ -54,12 +54,14 @@ for step in "$@"; do
     profile)
       timeout -k 10 1150 bash tools/profile_all.sh ${arg:-round} ${PROF_WL:-$BENCH_WL fast:bunny-primary-1024x768} || exit 1
       ls $O/profiles ;;
-    readme)
+    readme)   # every README cell on the package's saved schedules (no per-cell locks — the
+              # table reports what a user of the shipped table gets): the README cells' BVHs tuned into a copy of
+              # the package table (cells of one BVH and batch size share one entry, the last tuned), then measured
       cp gpu-ray-tracing_amd/mrt/tuned_schedules.json $O/tuned_schedules_all.json
       W=$(python3 -c "import sys; sys.path.insert(0,'tools'); import readme_table as r; print(' '.join('--workload '+c[0] for c in r.CELLS))")
       timeout -k 10 900 python -u tools/tune_db.py $W --rounds 2 --launches 10 --out $O/tuned_schedules_all.json \
-        --out-cells $O/tuned_cells.json > $O/tune_db_readme.txt 2> $O/tune_db_readme.err || fail "tune readme" $O/tune_db_readme.err
-      timeout -k 10 900 python -u tools/readme_table.py --tune-db $O/tuned_schedules_all.json --cell-db $O/tuned_cells.json \
+        > $O/tune_db_readme.txt 2> $O/tune_db_readme.err || fail "tune readme" $O/tune_db_readme.err
+      timeout -k 10 900 python -u tools/readme_table.py --tune-db $O/tuned_schedules_all.json \
         > $O/readme_table.log 2>&1 \
         || fail "readme table" $O/readme_table.log
       cat $O/readme_table.md ;;

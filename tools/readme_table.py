@@ -137,6 +137,11 @@ def main():
             "per_ray": {"nodes": round(n_nodes / batches.rays_traced, 2), "tris": round(n_tris / batches.rays_traced, 2)},
             "alg_gbs": round(alg_bytes / (kernel_ms * 1e-3) / 1e9, 1),
             "schedule": bench.schedule_of(tracer, batches.batches[0][0], True)["name"],
+            # the saved schedules the cell ran (checked against the shipped table by
+            # tests/test_readme_table.py): the BVH's fingerprint and its entries for the cell's batch sizes
+            "fingerprint": e["gbvh"].fingerprint,
+            "schedules": sorted({tuple(x[:3]) for x in tracer.schedules()
+                                 if x[0] in {rb.size for rb, _ in batches.batches}}),
             "parity_rays": n, "parity_all_rays": n == batches.rays_traced, "parity_agree": agree, "parity_kind": "valid hits" if any_hit else "id+t exact",
             "any_hit_results_reverified": checked if any_hit else None,
             "parity_same": same, "exact_t_ties": None if any_hit else ties,
