@@ -214,6 +214,18 @@ __global__ __launch_bounds__(kThreads) void block_live_kernel(ShardArgs a) {
     }
 }
 
+// Inclusive prefix sum over a wave's 64 lanes in six DPP adds (row_shr 1/2/4/8 within each
+// 16-lane row, then row_bcast 15/31 across rows): VALU only, no LDS permutes.
+__device__ inline int wave_scan_incl(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);   // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);   // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
 __global__ __launch_bounds__(kOrderThreads) void block_order_kernel(ShardArgs a) {
     constexpr int kWaves = kOrderThreads / 64;
     __shared__ uint16_t key[kOrderMax];
@@ -247,12 +259,7 @@ __global__ __launch_bounds__(kOrderThreads) void block_order_kernel(ShardArgs a)
         int pre[16];
 #pragma unroll
         for (int e = 0; e < 16; e++) {
-            int v = c[e];
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const int u = __shfl_up(v, off, 64);
-                if (lane >= off) v += u;
-            }
+            const int v = wave_scan_incl(c[e]);
             pre[e] = v - c[e];
             if (lane == 63) waveTot[wave][e] = v;
         }
@@ -262,14 +269,9 @@ __global__ __launch_bounds__(kOrderThreads) void block_order_kernel(ShardArgs a)
             for (int e0 = 0; e0 < 16 * kWaves; e0 += 64) {
                 const int q = e0 + lane, e = q / kWaves, w = q - e * kWaves;
                 const int v = waveTot[w][e];
-                int incl = v;
-#pragma unroll
-                for (int off = 1; off < 64; off <<= 1) {
-                    const int u = __shfl_up(incl, off, 64);
-                    if (lane >= off) incl += u;
-                }
+                const int incl = wave_scan_incl(v);
                 wavePre[w][e] = run + incl - v;
-                run += __shfl(incl, 63, 64);
+                run += __builtin_amdgcn_readlane(incl, 63);
             }
         }
         __syncthreads();

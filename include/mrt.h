@@ -139,7 +139,9 @@ typedef struct mrt_launch_cfg {
                                   at 20 waves/CU) deals each workgroup's 256 consecutive rays to its four
                                   waves by direction octant, degenerate (tmax < 0) rays last, instead of
                                   the strided deal (exact 4-wide traversal only); 0 = off (default; -1 =
-                                  default). Results are unchanged: every ray is traced once either way */
+                                  default). Results are unchanged: every ray is traced once either way.
+                                  With ray_sort = 1 the strided deal ignores lane_groups (in every launch,
+                                  also one whose batch needs several rounds, where the sort is skipped) */
     int32_t queue_xcc_mask;    /* test hook, 0 = off (default; -1 = default): 1..15 = a wave takes from queue
                                   (XCC_ID & mask) % num_queues, so with mask 3 and 8 queues, queues 4..7
                                   have no waves of their own (the unserved-queue sweep must trace them) */
