@@ -106,3 +106,40 @@ def test_secondary_hint_travels_with_the_buffer():
     assert rb.view(2, 5).secondary
     assert Tracer.flags(None, rb) & _lib.MRT_TRACE_SECONDARY
     assert not Tracer.flags(None, RayBuffer(torch.zeros((8, 8)), device=cpu)) & _lib.MRT_TRACE_SECONDARY
+
+
+def test_shard_blocks_size_query_and_argument_checks():
+    """mrt_shard_blocks / mrt_raygen_ao_blocks host-side contract (no device needed): the
+    block/ray counts of a rank's shard come back without touching the device (blocks NULL),
+    including the frame's partial last block; bad arguments are refused before any launch."""
+    import ctypes as C
+    from mrt import _lib
+    lib = _lib.trace_lib()
+    n, m = C.c_int32(0), C.c_int64(0)
+    # 1920x1080 at 8 spp in 1024-ray blocks: 16 200 blocks, 2 025 per rank of 8
+    assert lib.mrt_shard_blocks(None, 1920 * 1080, 8, 1024, 8, 3, 1, None, 0, C.byref(n), C.byref(m), None) == 0
+    assert (n.value, m.value) == (2025, 2025 * 1024)
+    # 97x61 primaries x 3 samples = 17 751 rays in 128-ray blocks: 139 blocks, the last 87 rays long
+    for rank, blocks in ((0, 70), (1, 69)):
+        assert lib.mrt_shard_blocks(None, 97 * 61, 3, 128, 2, rank, 0, None, 0, C.byref(n), C.byref(m), None) == 0
+        assert n.value == blocks
+        assert m.value == blocks * 128 - (128 - 17751 % 128 if rank == 0 else 0)
+    for bad in ((100, 1, 64, 0, 0, 1), (100, 1, 64, 2, 2, 1), (100, 0, 64, 1, 0, 1), (100, 1, 0, 1, 0, 1),
+                (100, 1, 64, 1, 0, 2), (-1, 1, 64, 1, 0, 1)):
+        np_, s, b, w, r, o = bad
+        assert lib.mrt_shard_blocks(None, np_, s, b, w, r, o, None, 0, C.byref(n), C.byref(m), None) == _lib.MRT_ERR_INVALID_ARG
+    # a capacity below the shard's blocks, and a live-first order over more than 16 384 blocks per rank
+    dummy = C.c_void_p(1)
+    assert lib.mrt_shard_blocks(dummy, 1000, 1, 64, 1, 0, 0, dummy, 3, C.byref(n), C.byref(m), None) == 5
+    assert lib.mrt_shard_blocks(dummy, 1 << 20, 8, 256, 1, 0, 1, dummy, 1 << 20, C.byref(n), C.byref(m), None) == 5
+    seeds = (C.c_uint32 * 1)(1804289383)
+    sp = C.cast(seeds, C.c_void_p)
+    # nothing listed: no launch; more blocks listed than the frame has, or a wrong ray count: refused
+    assert lib.mrt_raygen_ao_blocks(None, None, 100, None, 0, 2, 5.0, sp, 1, 1000, None, 0, 64, 0, None, None) == 0
+    assert lib.mrt_raygen_ao_blocks(dummy, dummy, 100, None, 0, 2, 5.0, sp, 1, 1000, dummy, 5, 64, 5 * 64,
+                                    dummy, None) == _lib.MRT_ERR_INVALID_ARG
+    assert lib.mrt_raygen_ao_blocks(dummy, dummy, 100, None, 0, 2, 5.0, sp, 1, 1000, dummy, 2, 64, 2 * 64 + 1,
+                                    dummy, None) == _lib.MRT_ERR_INVALID_ARG
+    # fewer seeds than the frame's batches (100 inputs at 30 per batch: 4 batches)
+    assert lib.mrt_raygen_ao_blocks(dummy, dummy, 100, None, 0, 2, 5.0, sp, 1, 30, dummy, 1, 64, 64,
+                                    dummy, None) == _lib.MRT_ERR_INVALID_ARG
