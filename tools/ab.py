@@ -97,7 +97,8 @@ def run(args, workload):
         for spec, lib, h in variants:
             launches = []
             for rb, _ in b.batches:
-                flags = (0 if rb.need_closest_hit else _lib.MRT_TRACE_ANY_HIT) | (0 if args.fast_rcp else _lib.MRT_TRACE_EXACT_RCP)
+                flags = ((0 if rb.need_closest_hit else _lib.MRT_TRACE_ANY_HIT) | (0 if args.fast_rcp else _lib.MRT_TRACE_EXACT_RCP)
+                         | (_lib.MRT_TRACE_SECONDARY if getattr(rb, "secondary", False) else 0))   # the ray class's schedules
                 launches.append((rb.rays.data_ptr(), rb.results.data_ptr(), rb.size, flags))
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda.synchronize()
