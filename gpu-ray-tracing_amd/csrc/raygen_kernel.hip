@@ -123,7 +123,8 @@ __global__ __launch_bounds__(kThreads) void ao_blocks_kernel(AOBlocksArgs a) {
     if (j >= a.outRays) return;
     const int64_t k = j / a.blockRays;
     const int64_t g = (int64_t)a.blocks[k] * a.blockRays + (j - k * a.blockRays);
-    if (g >= a.totalRays) return;   // past the frame's end: only the (last-listed) partial block
+    // past the frame's end: the (last-listed) partial block; a block id outside the frame writes nothing
+    if (g < 0 || g >= a.totalRays) return;
     const int p = (int)(g / a.numSamples), i = (int)(g - (int64_t)p * a.numSamples);
     const int batch = p / a.batchInputs;
     const int2 res = a.inResults[2 * p];
@@ -134,7 +135,7 @@ __global__ __launch_bounds__(kThreads) void ao_blocks_kernel(AOBlocksArgs a) {
 
 // The same rays when a workgroup's kTileRays outputs lie inside one block (blockRays a
 // multiple of kTileRays) and hold whole input rays (numSamples divides kTileRays, at most
-// kThreads of them): each input ray's basis (two trig calls, a normalize, the hash, three
+// kThreads input rays and at most kThreads samples per ray): each input ray's basis (two trig calls, a normalize, the hash, three
 // dependent loads) is computed once by one thread and each sample's hemisphere point once
 // per sample index, both through LDS — not once per output ray (S = 8: 8x fewer basis
 // evaluations) — then each thread writes kTileRays / kThreads rays (coalesced). Same
@@ -148,6 +149,7 @@ __global__ __launch_bounds__(kThreads) void ao_blocks_tiled_kernel(AOBlocksArgs 
     const int64_t j0 = (int64_t)blockIdx.x * kTileRays;
     const int64_t k = j0 / a.blockRays;
     const int64_t g0 = (int64_t)a.blocks[k] * a.blockRays + (j0 - k * a.blockRays);   // a multiple of S
+    if (g0 < 0 || g0 >= a.totalRays) return;   // a block id outside the frame (workgroup-uniform): nothing
     const int S = a.numSamples;
     const int perWg = kTileRays / S;
     const int p0 = (int)(g0 / S);
@@ -532,7 +534,8 @@ int mrt_raygen_ao_blocks(const void* inRays, const void* inResults, int32_t numI
     a.blocks = blocks;
     a.out = static_cast<rg::RayRec*>(outRays);
     for (int64_t k = 0; k < needBatches; k++) a.seeds[k] = batchSeeds[k];
-    if (blockRays % kTileRays == 0 && kTileRays % numSamples == 0 && kTileRays / numSamples <= kThreads)
+    if (blockRays % kTileRays == 0 && kTileRays % numSamples == 0 && kTileRays / numSamples <= kThreads &&
+        numSamples <= kThreads)   // the tile's input rays and its sample points each fit one LDS slot per thread
         hipLaunchKernelGGL(ao_blocks_tiled_kernel, dim3((unsigned)((numOutRays + kTileRays - 1) / kTileRays)),
                            dim3(kThreads), 0, static_cast<hipStream_t>(stream), a);
     else

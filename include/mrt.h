@@ -291,7 +291,9 @@ int  mrt_raygen_ao(const void* inRays, const void* inResults, int32_t numInputRa
  * batches hold there (mrt_raygen_ao of batch k). blocks: device int32[numBlocks], any
  * order (e.g. a rank's shard, its costly blocks first). Only the frame's last block can
  * be partial; when listed it must be the last entry, and numOutRays = the listed rays
- * ((numBlocks-1)*blockRays + its length; else numBlocks*blockRays). At most 256 batches. */
+ * ((numBlocks-1)*blockRays + its length; else numBlocks*blockRays). At most 256 batches.
+ * A block id outside [0, blocks in the frame) is not checked on the host (the list is device
+ * memory): its output rays are left unwritten. */
 int  mrt_raygen_ao_blocks(const void* inRays, const void* inResults, int32_t numInputRays, const float* triNormals,
                           int64_t numTris, int32_t numSamples, float maxDist, const uint32_t* batchSeeds,
                           int32_t numBatches, int32_t batchInputRays, const int32_t* blocks, int32_t numBlocks,

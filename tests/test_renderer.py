@@ -154,6 +154,8 @@ def test_renderer_batches_equal_the_oracle(sponza, ray_type, samples, w, h):
     (2, 8, 320, 240, 1 << 16, 1024, 3),     # 10 batches; blocks a multiple of the samples
     (1, 3, 97, 61, 1 << 12, 100, 2),        # ragged: 3 samples, 100-ray blocks, a partial last block
     (2, 1, 160, 120, 1 << 21, 4096, 1),     # one batch, the whole frame live blocks first
+    (1, 256, 24, 16, 1 << 16, 2048, 2),     # the tiled generator at its sample limit (256 per input ray)
+    (2, 512, 16, 12, 1 << 21, 1024, 2),     # more samples than the tile's LDS slots: the per-ray generator
 ])
 def test_secondary_blocks_equal_the_frame_batches(sponza, ray_type, samples, w, h, max_batch, block, world):
     """Renderer.secondary_blocks (mrt_raygen_ao_blocks): each rank's shard of
